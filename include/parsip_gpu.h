@@ -1,0 +1,251 @@
+/*
+ * parsip_gpu.h — C-ABI of the MI355X (gfx950) BlobTree polygonizer.
+ *
+ * Drop-in boundary for Parsip's PS_SimdPoly hot path.  Every struct below is
+ * byte-identical to the reference SoA contract so a host that fills
+ * PS::SIMDPOLY::SOABlobPrims / SOABlobOps / SOABlobPrimMatrices can hand the
+ * same bytes to this library:
+ *
+ *   reference struct                          (Parsip100/PS_SimdPoly/include/)
+ *   SOABlobPrims        9,500 B  align 4      PS_Polygonizer.h:98-130
+ *   SOABlobOps          5,636 B  align 4      PS_Polygonizer.h:134-154
+ *   SOABlobPrimMatrices 6,148 B  align 4      PS_Polygonizer.h:161-165
+ *   SOABlobBoxMatrices  8,196 B  align 4      PS_Polygonizer.h:171-175
+ *   MPU                21,524 B  align 4      PS_Polygonizer.h:183-195
+ *
+ * Entry points (each one cites the reference interface it replaces):
+ *   psgpu_count_mpus        <- CountMPUNeeded   PS_Polygonizer.h:384, .cpp:388-412
+ *   psgpu_prepare_bboxes    <- PrepareBBoxes    PS_Polygonizer.h:385, .cpp:55-309
+ *   psgpu_polygonize_mpus   <- Polygonize       PS_Polygonizer.h:386-391, .cpp:315-385
+ *                              (blocking, fills the caller's PolyMPUs layout)
+ *   psgpu_create/destroy/set_model/polygonize/finish/...
+ *                           <- the same Polygonize split into a device-resident,
+ *                              stream-ordered form (compact mesh stays in HBM)
+ *   psgpu_translate_blobtree_type <- enum map for SimdPoly::linearizeBlobTree
+ *                              (PS_HighPerformanceRender.cpp:42-364; _constSettings.h:26-38)
+ *
+ * Error codes keep PS_Polygonizer.h:47-50 and add explicit overflow / device codes
+ * (the reference truncates at MAX_MPU_COUNT with only a printf, .cpp:355-356, and
+ * never checks the 512 vertex / triangle per-MPU capacity, .cpp:785-824).
+ *
+ * No torch / HIP types appear in these signatures: streams are passed as void*
+ * (a hipStream_t, NULL = the context's own stream).
+ */
+#ifndef PARSIP_GPU_H
+#define PARSIP_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants (PS_Polygonizer.h:21-81) ---------------------------------- */
+#define PSGPU_GRID_DIM              8      /* corners per MPU axis (GRID_DIM_8)   */
+#define PSGPU_CELLS_PER_MPU         7
+#define PSGPU_ISO_VALUE             0.5f
+#define PSGPU_ISO_DIST              0.45420206f
+#define PSGPU_NORMAL_DELTA          0.001f
+#define PSGPU_MIN_CELL_SIZE         0.01f
+#define PSGPU_MAX_TREE_NODES        128
+#define PSGPU_PRIM_MATRIX_STRIDE    12
+#define PSGPU_BOX_MATRIX_STRIDE     16
+#define PSGPU_MAX_MPU_COUNT         24000  /* the reference PolyMPUs capacity     */
+#define PSGPU_MAX_MPU_VERTEX_COUNT  512
+#define PSGPU_MAX_MPU_TRIANGLE_COUNT 512
+
+/* ---- return codes -------------------------------------------------------- */
+#define PSGPU_RET_SUCCESS          1   /* RET_SUCCESS                              */
+#define PSGPU_RET_PARAM_ERROR     -1   /* RET_PARAM_ERROR (ctPrims == 0, bad args) */
+#define PSGPU_RET_NOT_ENOUGH_MEM  -2   /* RET_NOT_ENOUGH_MEM (device alloc failed)  */
+#define PSGPU_RET_INVALID_BVH     -3   /* RET_INVALID_BVH (op tree not a tree)      */
+#define PSGPU_RET_MPU_OVERFLOW    -4   /* more MPUs than the caller's capacity      */
+#define PSGPU_RET_MPU_VT_OVERFLOW -5   /* an MPU exceeds 512 vertices / triangles   */
+#define PSGPU_RET_DEVICE_ERROR    -6   /* HIP / RCCL runtime error                  */
+
+/* ---- node types: the hot path's own ordering (PS_Polygonizer.h:84-91) ---- */
+enum PsNodeType {
+    PSGPU_PRIM_CYLINDER = 0, PSGPU_PRIM_DISC = 1, PSGPU_PRIM_LINE = 2, PSGPU_PRIM_POINT = 3,
+    PSGPU_PRIM_RING = 4, PSGPU_PRIM_POLYGON = 5, PSGPU_PRIM_CUBE = 6, PSGPU_PRIM_TRIANGLE = 7,
+    PSGPU_PRIM_CATMULLROM = 8, PSGPU_PRIM_SKELETON = 9, PSGPU_PRIM_QUADRICPOINT = 10,
+    PSGPU_PRIM_FASTQPS = 11, PSGPU_PRIM_HALFPLANE = 12, PSGPU_PRIM_NULL = 13,
+    PSGPU_OP_UNION = 14, PSGPU_OP_INTERSECT = 15, PSGPU_OP_DIF = 16, PSGPU_OP_SMOOTHDIF = 17,
+    PSGPU_OP_BLEND = 18, PSGPU_OP_RICCIBLEND = 19, PSGPU_OP_GRADIENTBLEND = 20,
+    PSGPU_OP_AFFINE = 21, PSGPU_OP_WARPTWIST = 22, PSGPU_OP_WARPTAPER = 23,
+    PSGPU_OP_WARPBEND = 24, PSGPU_OP_WARPSHEAR = 25, PSGPU_OP_CACHE = 26,
+    PSGPU_OP_TEXTURE = 27, PSGPU_OP_PCM = 28
+};
+
+/* ---- SoA model (byte-exact) ---------------------------------------------- */
+typedef struct PsVec3f { float x, y, z; } PsVec3f;
+
+typedef struct PsSoaBlobPrims {          /* SOABlobPrims, PS_Polygonizer.h:98-130 */
+    float posX[128], posY[128], posZ[128];
+    float dirX[128], dirY[128], dirZ[128];
+    float resX[128], resY[128], resZ[128];
+    float colorX[128], colorY[128], colorZ[128];
+    float vPrimBoxLoX[128], vPrimBoxLoY[128], vPrimBoxLoZ[128];
+    float vPrimBoxHiX[128], vPrimBoxHiY[128], vPrimBoxHiZ[128];
+    uint8_t skeletType[128];
+    uint8_t idxMatrix[128];
+    PsVec3f bboxLo;
+    PsVec3f bboxHi;
+    uint32_t ctPrims;
+} PsSoaBlobPrims;
+
+typedef struct PsSoaBlobOps {            /* SOABlobOps, PS_Polygonizer.h:134-154 */
+    uint8_t opType[128];
+    uint8_t opLeftChild[128];
+    uint8_t opRightChild[128];
+    uint8_t opChildKind[128];            /* bit1: left is op, bit0: right is op  */
+    float vBoxLoX[128], vBoxLoY[128], vBoxLoZ[128];
+    float vBoxHiX[128], vBoxHiY[128], vBoxHiZ[128];
+    float resX[128], resY[128], resZ[128], resW[128];
+    uint32_t ctOps;
+} PsSoaBlobOps;
+
+typedef struct PsSoaPrimMatrices {       /* SOABlobPrimMatrices, :161-165 (row 0 = identity) */
+    float matrix[128 * PSGPU_PRIM_MATRIX_STRIDE];
+    uint32_t count;
+} PsSoaPrimMatrices;
+
+typedef struct PsSoaBoxMatrices {        /* SOABlobBoxMatrices, :171-175 */
+    float matrix[128 * PSGPU_BOX_MATRIX_STRIDE];
+    uint32_t count;
+} PsSoaBoxMatrices;
+
+typedef struct PsMPU {                   /* MPU, PS_Polygonizer.h:183-195 */
+    float vPos[PSGPU_MAX_MPU_VERTEX_COUNT * 3];
+    float vNorm[PSGPU_MAX_MPU_VERTEX_COUNT * 3];
+    float vColor[PSGPU_MAX_MPU_VERTEX_COUNT * 3];
+    uint16_t triangles[PSGPU_MAX_MPU_TRIANGLE_COUNT * 3];
+    uint16_t ctVertices;
+    uint16_t ctTriangles;
+    PsVec3f bboxLo;
+    uint32_t ctFieldEvals;
+} PsMPU;
+
+/* Per-MPU statistics (replaces MPUSTATS, PS_Polygonizer.h:201-207: GPU work has no
+ * thread id / tick pair, so the export is the per-MPU outcome instead). */
+typedef struct PsMpuStats {
+    uint32_t passedPrecheck;   /* S1 (8-corner F>0 test) passed                  */
+    uint32_t ctFieldEvals;     /* 128 if S1 passed else 0 (reference counter)     */
+    uint32_t ctVertices;
+    uint32_t ctTriangles;
+} PsMpuStats;
+
+/* Result summary of one polygonization. */
+typedef struct PsMeshInfo {
+    uint32_t ctMPUs;            /* MPUs in the processed range                     */
+    uint32_t ctPassedPrecheck;  /* MPUs that passed S1                              */
+    uint32_t ctSurfaceMPUs;     /* MPUs that produced >= 1 triangle                 */
+    uint32_t ctVertices;
+    uint32_t ctTriangles;
+    int32_t  firstOverflowMPU;  /* global MPU id with > 512 V or T, or -1           */
+    uint64_t ctLaneEvals;       /* field evaluations performed (per point)          */
+} PsMeshInfo;
+
+/* Device-resident compact mesh of the last polygonization (pointers into the
+ * context's HBM buffers; valid until the next psgpu_polygonize on the context).
+ * Vertices of MPU w occupy [mpuVertexOffset[w], mpuVertexOffset[w]+ct) in MPU order,
+ * i.e. exactly the reference's concatenation of vMPUs[i].vPos over i.              */
+typedef struct PsMeshDevice {
+    const float*    pos;              /* ctVertices * 3, xyz interleaved           */
+    const float*    nrm;              /* ctVertices * 3                            */
+    const float*    col;              /* ctVertices * 3                            */
+    const uint32_t* tris;             /* ctTriangles * 3, global vertex ids        */
+    const uint32_t* surfaceMpuIds;    /* ctPassedPrecheck: global MPU id per slot  */
+    const uint32_t* mpuVertexOffset;  /* ctPassedPrecheck + 1 (exclusive scan)     */
+    const uint32_t* mpuTriangleOffset;/* ctPassedPrecheck + 1                      */
+} PsMeshDevice;
+
+typedef struct psgpu_ctx psgpu_ctx;
+
+/* ---- host-only helpers --------------------------------------------------- */
+/* CountMPUNeeded (PS_Polygonizer.cpp:388-412). */
+uint32_t psgpu_count_mpus(float cellsize, const float lo[3], const float hi[3]);
+/* MPU lattice dimensions along x,y,z (PS_Polygonizer.cpp:339-352). */
+int psgpu_mpu_dims(float cellsize, const PsSoaBlobPrims* prims, uint32_t dims[3]);
+/* PrepareBBoxes (PS_Polygonizer.cpp:55-309) with the exact iso distance
+ * PSGPU_ISO_DIST instead of the reference's undefined-behaviour FastSqrt. */
+int psgpu_prepare_bboxes(float cellsize, PsSoaBlobPrims* prims, PsSoaBoxMatrices* boxMatrices,
+                         PsSoaBlobOps* ops);
+/* _constSettings.h:26-38 code (caller / PS_BlobTree side) -> PsNodeType; -1 if none. */
+int psgpu_translate_blobtree_type(int blobtreeType);
+/* Marching-cubes triangle table (256 x 16, -1 padded), generated at load time. */
+void psgpu_tritable(int32_t out[256 * 16]);
+/* Library version string. */
+const char* psgpu_version(void);
+
+/* ---- device context ------------------------------------------------------ */
+int  psgpu_create(int deviceOrdinal, psgpu_ctx** out);
+void psgpu_destroy(psgpu_ctx* ctx);
+int  psgpu_device_count(void);
+/* Upload a model (validates the op tree; builds the device walk program). */
+int  psgpu_set_model(psgpu_ctx* ctx, const PsSoaBlobPrims* prims,
+                     const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops);
+/* Enqueue a polygonization of global MPUs [mpuBegin, mpuEnd) (clamped to the
+ * lattice; pass 0, UINT32_MAX for all) on `stream` (hipStream_t or NULL). Async. */
+int  psgpu_polygonize(psgpu_ctx* ctx, float cellsize, uint32_t mpuBegin, uint32_t mpuEnd,
+                      void* stream);
+/* Wait for the last polygonize and report counts / errors.  If the output
+ * buffers were too small the call re-runs the polygonization with grown buffers. */
+int  psgpu_finish(psgpu_ctx* ctx, PsMeshInfo* info);
+int  psgpu_mesh_device(psgpu_ctx* ctx, PsMeshDevice* out);
+/* Copy the compact mesh to host arrays (any pointer may be NULL). */
+int  psgpu_download_mesh(psgpu_ctx* ctx, float* pos, float* nrm, float* col, uint32_t* tris,
+                         uint32_t* surfaceMpuIds, uint32_t* mpuVertexOffset,
+                         uint32_t* mpuTriangleOffset);
+/* Per-MPU stats for every MPU in the last processed range (ctMPUs entries). */
+int  psgpu_download_stats(psgpu_ctx* ctx, PsMpuStats* stats);
+/* Scatter the last result into the reference PolyMPUs layout (vMPUs[0..ctMPUs)). */
+int  psgpu_export_polympus(psgpu_ctx* ctx, PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs);
+/* Blocking drop-in for PS::SIMDPOLY::Polygonize: upload, run, export. */
+int  psgpu_polygonize_mpus(psgpu_ctx* ctx, float cellsize, const PsSoaBlobPrims* prims,
+                           const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops,
+                           PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs,
+                           PsMpuStats* statsOrNull);
+/* Device-side timing of the last polygonize, per kernel (ms); returns count filled. */
+int  psgpu_last_kernel_times(psgpu_ctx* ctx, float* ms, int maxKernels, const char** names);
+/* FieldComputer::fieldValue / fieldValueAndColor on n host points (xyz interleaved):
+ * mode 0 = consecutive points form the reference's 4-lane pruning groups,
+ * mode 1 = every point alone (4 identical lanes), mode 2 = mode 1 + colour (n*3). */
+int  psgpu_field_values(psgpu_ctx* ctx, const float* xyz, uint32_t n, int mode, float* out, float* colOut);
+/* Set a context option (see PSGPU_OPT_*). */
+int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
+#define PSGPU_OPT_KERNEL_TIMING 1   /* 1: record hipEvents around every kernel */
+#define PSGPU_OPT_CULLING       2   /* 1: exact per-wave primitive culling (default) */
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#ifdef __cplusplus
+static_assert(sizeof(PsSoaBlobPrims) == 9500, "SOABlobPrims size");
+static_assert(offsetof(PsSoaBlobPrims, skeletType) == 9216, "skeletType offset");
+static_assert(offsetof(PsSoaBlobPrims, idxMatrix) == 9344, "idxMatrix offset");
+static_assert(offsetof(PsSoaBlobPrims, bboxLo) == 9472, "bboxLo offset");
+static_assert(offsetof(PsSoaBlobPrims, ctPrims) == 9496, "ctPrims offset");
+static_assert(sizeof(PsSoaBlobOps) == 5636, "SOABlobOps size");
+static_assert(offsetof(PsSoaBlobOps, vBoxLoX) == 512, "vBoxLoX offset");
+static_assert(offsetof(PsSoaBlobOps, resX) == 3584, "resX offset");
+static_assert(offsetof(PsSoaBlobOps, ctOps) == 5632, "ctOps offset");
+static_assert(sizeof(PsSoaPrimMatrices) == 6148, "SOABlobPrimMatrices size");
+static_assert(sizeof(PsSoaBoxMatrices) == 8196, "SOABlobBoxMatrices size");
+static_assert(sizeof(PsMPU) == 21524, "MPU size");
+static_assert(offsetof(PsMPU, vNorm) == 6144, "vNorm offset");
+static_assert(offsetof(PsMPU, vColor) == 12288, "vColor offset");
+static_assert(offsetof(PsMPU, triangles) == 18432, "triangles offset");
+static_assert(offsetof(PsMPU, ctVertices) == 21504, "ctVertices offset");
+static_assert(offsetof(PsMPU, bboxLo) == 21508, "MPU bboxLo offset");
+static_assert(offsetof(PsMPU, ctFieldEvals) == 21520, "ctFieldEvals offset");
+#else
+_Static_assert(sizeof(PsSoaBlobPrims) == 9500, "SOABlobPrims size");
+_Static_assert(sizeof(PsSoaBlobOps) == 5636, "SOABlobOps size");
+_Static_assert(sizeof(PsSoaPrimMatrices) == 6148, "SOABlobPrimMatrices size");
+_Static_assert(sizeof(PsSoaBoxMatrices) == 8196, "SOABlobBoxMatrices size");
+_Static_assert(sizeof(PsMPU) == 21524, "MPU size");
+#endif
+
+#endif /* PARSIP_GPU_H */

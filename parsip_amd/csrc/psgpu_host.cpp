@@ -1,0 +1,834 @@
+// psgpu_host.cpp — C-ABI of the MI355X polygonizer (include/parsip_gpu.h).
+//
+// Host side of PS::SIMDPOLY::Polygonize (PS_Polygonizer.cpp:315-385): MPU lattice,
+// model upload (the reference's per-thread FieldComputer copy, :22-50, becomes one
+// 28 KB device image read through the scalar cache), kernel sequencing on one HIP
+// stream, and the exports back to the reference PolyMPUs layout.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/parsip_gpu.h"
+#include "psgpu_launch.h"
+#include "psgpu_model.h"
+
+using namespace psgpu;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Marching-cubes table.  Generated, not transcribed: Bloomenthal's cube-table
+// construction ("An Implicit Surface Polygonizer", Graphics Gems IV, 1994) walks
+// each sign-changing edge clockwise around the cube faces to build polygons; the
+// reference's g_triTableCache (_CellConfigTable.h:60-317) keeps polygons in
+// discovery order with each polygon's edges in reverse walk order and fans
+// triangles about the last edge.  Corner c: bit2 = x, bit1 = y, bit0 = z.
+struct CubeTables {
+    int8_t tri[256][16];
+    uint8_t ntri[256];
+    uint8_t corner1[12], corner2[12], axis[12];
+};
+
+const CubeTables& cube_tables() {
+    static CubeTables T;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        // edges LB LT LN LF RB RT RN RF BN BF TN TF; faces L R B T N F
+        static const uint8_t c1[12] = {0, 2, 0, 1, 4, 6, 4, 5, 0, 1, 2, 3};
+        static const uint8_t c2[12] = {1, 3, 2, 3, 5, 7, 6, 7, 4, 5, 6, 7};
+        static const uint8_t ax[12] = {2, 2, 1, 1, 2, 2, 1, 1, 0, 0, 0, 0};
+        static const uint8_t lface[12] = {2, 0, 0, 5, 1, 3, 4, 1, 4, 2, 3, 5};
+        static const uint8_t rface[12] = {0, 3, 4, 0, 2, 1, 1, 5, 2, 5, 4, 3};
+        // next clockwise edge around `face` after `edge`: {face of the edge's first
+        // listed face, next-if-that-face, next-otherwise}
+        static const uint8_t ccwFace[12] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3};
+        static const uint8_t nextOn[12] = {3, 2, 0, 1, 6, 7, 5, 4, 4, 0, 1, 5};
+        static const uint8_t nextOff[12] = {8, 11, 10, 9, 9, 10, 8, 11, 2, 7, 6, 3};
+        memcpy(T.corner1, c1, 12);
+        memcpy(T.corner2, c2, 12);
+        memcpy(T.axis, ax, 12);
+        for (int cfg = 0; cfg < 256; ++cfg) {
+            auto in = [cfg](int c) { return (cfg >> c) & 1; };
+            bool done[12] = {};
+            std::vector<int> rows;
+            for (int e = 0; e < 12; ++e) {
+                if (done[e] || in(c1[e]) == in(c2[e])) continue;
+                std::vector<int> poly;
+                int edge = e, face = in(c1[e]) ? rface[e] : lface[e];
+                for (;;) {
+                    edge = (face == ccwFace[edge]) ? nextOn[edge] : nextOff[edge];
+                    done[edge] = true;
+                    if (in(c1[edge]) != in(c2[edge])) {
+                        poly.insert(poly.begin(), edge);
+                        if (edge == e) break;
+                        face = (face == lface[edge]) ? rface[edge] : lface[edge];
+                    }
+                }
+                const int np = (int)poly.size();
+                for (int t = np - 3; t >= 0; --t) {
+                    rows.push_back(poly[t]);
+                    rows.push_back(poly[t + 1]);
+                    rows.push_back(poly[np - 1]);
+                }
+            }
+            for (int i = 0; i < 16; ++i) T.tri[cfg][i] = i < (int)rows.size() ? (int8_t)rows[i] : (int8_t)-1;
+            T.ntri[cfg] = (uint8_t)(rows.size() / 3);
+        }
+    });
+    return T;
+}
+
+// ---------------------------------------------------------------------------
+// Walk program: the reference's processing order of fieldValue's explicit stack.
+bool op_needs_left(int t) { return (t >= 14 && t <= 19) || (t >= 22 && t <= 25); }
+bool op_needs_right(int t) { return t >= 14 && t <= 19; }
+
+struct ProgramBuilder {
+    const PsSoaBlobOps& O;
+    std::vector<Instr> prog;
+    std::vector<uint8_t> seen;
+    int maxSlot = 0;
+    bool ok = true;
+
+    explicit ProgramBuilder(const PsSoaBlobOps& ops) : O(ops), seen(128, 0) {}
+
+    void emit(int op, int depth, int h) {
+        if (!ok) return;
+        if (op < 0 || op >= (int)O.ctOps || seen[op] || depth > 127 || h + 3 >= kMaxSlots) {
+            ok = false;
+            return;
+        }
+        seen[op] = 1;
+        const int kind = O.opChildKind[op];
+        const int L = O.opLeftChild[op], R = O.opRightChild[op];
+        const int type = O.opType[op];
+        size_t enterAt = 0;
+        if (depth > 3) {
+            Instr e{};
+            e.kind = kEnter;
+            e.idx = (uint16_t)op;
+            e.out = (uint8_t)h;
+            enterAt = prog.size();
+            prog.push_back(e);
+        }
+        int next = h, lslot = 0, rslot = 0;
+        if (kind & 1) {  // right op subtree first (pushed last, popped first)
+            emit(R, depth + 1, h);
+            rslot = h;
+            next = h + 1;
+        }
+        if (kind & 2) {
+            emit(L, depth + 1, next);
+            lslot = next;
+            next = next + 1;
+        }
+        if (!ok) return;
+        int freeSlot = next;
+        if (!(kind & 2) && op_needs_left(type)) {
+            if (L >= 128) { ok = false; return; }
+            Instr p{};
+            p.kind = kPrim;
+            p.idx = (uint16_t)L;
+            p.out = (uint8_t)freeSlot;
+            prog.push_back(p);
+            lslot = freeSlot++;
+        }
+        if (!(kind & 1) && op_needs_right(type)) {
+            if (R >= 128) { ok = false; return; }
+            Instr p{};
+            p.kind = kPrim;
+            p.idx = (uint16_t)R;
+            p.out = (uint8_t)freeSlot;
+            prog.push_back(p);
+            rslot = freeSlot++;
+        }
+        maxSlot = std::max(maxSlot, freeSlot);
+        Instr c{};
+        c.kind = kOp;
+        c.type = (uint8_t)type;
+        c.out = (uint8_t)h;
+        c.lslot = (uint8_t)lslot;
+        c.rslot = (uint8_t)rslot;
+        c.childKind = (uint8_t)kind;
+        c.L = (uint8_t)L;
+        c.R = (uint8_t)R;
+        c.idx = (uint16_t)op;
+        prog.push_back(c);
+        if (depth > 3) prog[enterAt].skipTo = (uint16_t)prog.size();
+        if (prog.size() > (size_t)kMaxInstr) ok = false;
+    }
+};
+
+bool finite3(const float* v) { return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]); }
+
+int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, const PsSoaBlobOps& O, DevModel& D) {
+    memset(&D, 0, sizeof(D));
+    if (P.ctPrims == 0 || P.ctPrims > 128 || O.ctOps > 128) return PSGPU_RET_PARAM_ERROR;
+    D.ctPrims = P.ctPrims;
+    D.ctOps = O.ctOps;
+    if (O.ctOps == 0) {
+        for (uint32_t i = 0; i < P.ctPrims; ++i) {
+            Instr s{};
+            s.kind = kSumPrim;
+            s.idx = (uint16_t)i;
+            D.instr[i] = s;
+        }
+        D.nInstr = P.ctPrims;
+        D.nSlots = 1;
+    } else {
+        ProgramBuilder b(O);
+        b.emit(0, 0, 0);
+        if (!b.ok) return PSGPU_RET_INVALID_BVH;
+        D.nInstr = (uint32_t)b.prog.size();
+        std::copy(b.prog.begin(), b.prog.end(), D.instr);
+        D.nSlots = (uint32_t)std::max(1, b.maxSlot);
+    }
+    for (uint32_t i = 0; i < 128; ++i) {
+        DevOp& d = D.ops[i];
+        d.lo[0] = O.vBoxLoX[i]; d.lo[1] = O.vBoxLoY[i]; d.lo[2] = O.vBoxLoZ[i];
+        d.hi[0] = O.vBoxHiX[i]; d.hi[1] = O.vBoxHiY[i]; d.hi[2] = O.vBoxHiZ[i];
+        d.resY = O.resY[i];
+        d.type = O.opType[i];
+    }
+    // every one of the 128 prim slots is uploaded: the reference evaluates whatever
+    // index an op names, even past ctPrims (SOABlobPrims keeps all 128 entries)
+    for (uint32_t i = 0; i < 128; ++i) {
+        DevPrim& d = D.prims[i];
+        d.pos[0] = P.posX[i]; d.pos[1] = P.posY[i]; d.pos[2] = P.posZ[i];
+        d.dir[0] = P.dirX[i]; d.dir[1] = P.dirY[i]; d.dir[2] = P.dirZ[i];
+        d.res[0] = P.resX[i]; d.res[1] = P.resY[i]; d.res[2] = P.resZ[i];
+        d.col[0] = P.colorX[i]; d.col[1] = P.colorY[i]; d.col[2] = P.colorZ[i];
+        d.type = P.skeletType[i];
+        const uint32_t im = P.idxMatrix[i];
+        d.hasMatrix = im != 0;
+        if (im != 0) {
+            if (im >= 128) return PSGPU_RET_PARAM_ERROR;
+            memcpy(d.mat, &Mx.matrix[im * PSGPU_PRIM_MATRIX_STRIDE], 12 * sizeof(float));
+        }
+        // exact-culling eligibility (see make_cull_mask in psgpu_kernels.hip)
+        bool c = !d.hasMatrix && finite3(d.pos);
+        switch (d.type) {
+        case PSGPU_PRIM_POINT: break;
+        case PSGPU_PRIM_LINE: {
+            const double ux = (double)d.dir[0] - d.pos[0], uy = (double)d.dir[1] - d.pos[1],
+                         uz = (double)d.dir[2] - d.pos[2];
+            c = c && finite3(d.dir) && (ux * ux + uy * uy + uz * uz) > 1e-6;
+        } break;
+        case PSGPU_PRIM_CUBE: c = c && std::isfinite(d.res[0]) && d.res[0] >= 0.0f; break;
+        case PSGPU_PRIM_CYLINDER: {
+            const double n2 = (double)d.dir[0] * d.dir[0] + (double)d.dir[1] * d.dir[1] + (double)d.dir[2] * d.dir[2];
+            c = c && finite3(d.dir) && std::fabs(n2 - 1.0) < 1e-4 && d.res[0] >= 0.0f && d.res[1] >= 0.0f &&
+                std::isfinite(d.res[0]) && std::isfinite(d.res[1]);
+        } break;
+        default: c = false; break;
+        }
+        d.cullable = c ? 1u : 0u;
+    }
+    return PSGPU_RET_SUCCESS;
+}
+
+void lattice_dims(float cs, const PsVec3f& lo, const PsVec3f& hi, uint32_t d[3]) {
+    const float ext[3] = {hi.x - lo.x, hi.y - lo.y, hi.z - lo.z};
+    for (int a = 0; a < 3; ++a) {
+        const float q = ext[a] / cs;
+        const int cells = (int)std::ceil(q);
+        int n = cells / PSGPU_CELLS_PER_MPU;
+        if (cells % PSGPU_CELLS_PER_MPU != 0) ++n;
+        d[a] = n > 0 ? (uint32_t)n : 0u;
+    }
+}
+
+template <typename T>
+hipError_t grow(T*& ptr, size_t& cap, size_t need) {
+    if (need <= cap && ptr) return hipSuccess;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    size_t n = std::max<size_t>(need, cap + cap / 2);
+    hipError_t e = hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T));
+    cap = e == hipSuccess ? n : 0;
+    return e;
+}
+
+constexpr int kNumKernels = 6;
+const char* kKernelNames[kNumKernels] = {"k_precheck", "k_compact", "k_mpu", "k_scan", "k_vertex", "k_tris"};
+
+}  // namespace
+
+struct psgpu_ctx {
+    int device = 0;
+    int numCUs = 256;
+    hipStream_t stream = nullptr;
+    PsSoaBlobPrims primsHost;  // bbox + counts of the current model
+    DevModel model{};
+    DevModel* dModel = nullptr;
+    bool haveModel = false;
+    int cull = 1;
+    int timing = 0;
+    // geometry of the last run
+    float cs = 0.0f;
+    uint32_t dims[3] = {0, 0, 0};
+    uint32_t mpuBegin = 0, mpuCount = 0;
+    hipStream_t runStream = nullptr;
+    bool pending = false;
+    bool haveResult = false;
+    // device buffers
+    size_t capMask = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
+    uint32_t* passMask = nullptr;
+    uint32_t* passList = nullptr;
+    uint2* counts = nullptr;
+    uint32_t* voff = nullptr;
+    uint32_t* toff = nullptr;
+    VertexRec* vq = nullptr;
+    TriRec* tq = nullptr;
+    float* pos = nullptr;
+    float* nrm = nullptr;
+    float* col = nullptr;
+    uint32_t* tris = nullptr;
+    DevCounters* ctr = nullptr;
+    uint32_t* dequeue = nullptr;
+    DevCounters* hostCtr = nullptr;  // pinned
+    DevCounters* initCtr = nullptr;  // pinned template
+    uint32_t vcap = 1u << 20, tcap = 1u << 21;
+    hipEvent_t ev[kNumKernels + 1] = {};
+    float lastMs[kNumKernels] = {};
+    PsMeshInfo info{};
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    if (e == hipSuccess) return PSGPU_RET_SUCCESS;
+    fprintf(stderr, "psgpu: %s failed: %s\n", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? PSGPU_RET_NOT_ENOUGH_MEM : PSGPU_RET_DEVICE_ERROR;
+}
+
+#define PSGPU_CHECK(expr)                                   \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);   \
+    } while (0)
+
+int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
+    const size_t n = std::max<uint32_t>(mpuCount, 1);
+    PSGPU_CHECK(grow(c->passMask, c->capMask, (n + 31) / 32));
+    PSGPU_CHECK(grow(c->passList, c->capList, n));
+    PSGPU_CHECK(grow(c->counts, c->capCounts, n));
+    size_t capOff2 = c->capOff;
+    PSGPU_CHECK(grow(c->voff, c->capOff, n + 1));
+    PSGPU_CHECK(grow(c->toff, capOff2, n + 1));
+    PSGPU_CHECK(grow(c->vq, c->capVq, c->vcap));
+    PSGPU_CHECK(grow(c->tq, c->capTq, c->tcap));
+    size_t capV2 = c->capV, capV3 = c->capV;
+    PSGPU_CHECK(grow(c->pos, c->capV, (size_t)c->vcap * 3));
+    PSGPU_CHECK(grow(c->nrm, capV2, (size_t)c->vcap * 3));
+    PSGPU_CHECK(grow(c->col, capV3, (size_t)c->vcap * 3));
+    PSGPU_CHECK(grow(c->tris, c->capT, (size_t)c->tcap * 3));
+    return PSGPU_RET_SUCCESS;
+}
+
+Params make_params(psgpu_ctx* c) {
+    Params p{};
+    p.model = c->dModel;
+    p.cs = c->cs;
+    p.side = c->cs * (float)PSGPU_CELLS_PER_MPU;
+    p.lo[0] = c->primsHost.bboxLo.x;
+    p.lo[1] = c->primsHost.bboxLo.y;
+    p.lo[2] = c->primsHost.bboxLo.z;
+    for (int a = 0; a < 3; ++a) p.dims[a] = c->dims[a];
+    p.mpuBegin = c->mpuBegin;
+    p.mpuCount = c->mpuCount;
+    p.cull = (uint32_t)c->cull;
+    p.passMask = c->passMask;
+    p.passList = c->passList;
+    p.counts = c->counts;
+    p.voff = c->voff;
+    p.toff = c->toff;
+    p.vq = c->vq;
+    p.vcap = c->vcap;
+    p.tq = c->tq;
+    p.tcap = c->tcap;
+    p.pos = c->pos;
+    p.nrm = c->nrm;
+    p.col = c->col;
+    p.tris = c->tris;
+    p.ctr = c->ctr;
+    p.dequeue = c->dequeue;
+    p.slotsPerLane = c->model.nSlots;
+    return p;
+}
+
+int enqueue(psgpu_ctx* c, hipStream_t s) {
+    Params p = make_params(c);
+    PSGPU_CHECK(hipMemcpyAsync(c->ctr, c->initCtr, sizeof(DevCounters), hipMemcpyHostToDevice, s));
+    PSGPU_CHECK(hipMemsetAsync(c->dequeue, 0, 4 * sizeof(uint32_t), s));
+    const bool t = c->timing != 0;
+    const uint32_t persist = (uint32_t)c->numCUs * 4;
+    if (t) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
+    if (c->mpuCount > 0) {
+        PSGPU_CHECK(launch_precheck(p, s));
+        if (t) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
+        PSGPU_CHECK(launch_compact(p, s));
+        if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
+        PSGPU_CHECK(launch_mpu(p, s));
+        if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
+        PSGPU_CHECK(launch_scan(p, s));
+        if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
+        PSGPU_CHECK(launch_vertex(p, s, persist));
+        if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
+        PSGPU_CHECK(launch_tris(p, s, persist));
+        if (t) PSGPU_CHECK(hipEventRecord(c->ev[6], s));
+    }
+    PSGPU_CHECK(hipMemcpyAsync(c->hostCtr, c->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+    return PSGPU_RET_SUCCESS;
+}
+
+int set_device(psgpu_ctx* c) { return hip_fail(hipSetDevice(c->device), "hipSetDevice"); }
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* psgpu_version(void) { return "parsip_amd 0.1 (gfx950)"; }
+
+void psgpu_tritable(int32_t out[256 * 16]) {
+    const CubeTables& T = cube_tables();
+    for (int c = 0; c < 256; ++c)
+        for (int i = 0; i < 16; ++i) out[c * 16 + i] = T.tri[c][i];
+}
+
+uint32_t psgpu_count_mpus(float cellsize, const float lo[3], const float hi[3]) {
+    if (!(cellsize > 0.0f)) return 0;
+    PsVec3f l{lo[0], lo[1], lo[2]}, h{hi[0], hi[1], hi[2]};
+    uint32_t d[3];
+    lattice_dims(cellsize, l, h, d);
+    return d[0] * d[1] * d[2];
+}
+
+int psgpu_mpu_dims(float cellsize, const PsSoaBlobPrims* prims, uint32_t dims[3]) {
+    if (!prims || !(cellsize > 0.0f)) return PSGPU_RET_PARAM_ERROR;
+    lattice_dims(cellsize, prims->bboxLo, prims->bboxHi, dims);
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_translate_blobtree_type(int t) {
+    // _constSettings.h:26-38 -> PS_Polygonizer.h:84-91
+    static const int map[29] = {
+        PSGPU_PRIM_POINT, PSGPU_PRIM_LINE, PSGPU_PRIM_CYLINDER, PSGPU_PRIM_DISC, PSGPU_PRIM_RING,
+        PSGPU_PRIM_POLYGON, PSGPU_PRIM_CUBE, PSGPU_PRIM_TRIANGLE, PSGPU_PRIM_CATMULLROM, PSGPU_PRIM_SKELETON,
+        PSGPU_PRIM_QUADRICPOINT, PSGPU_PRIM_HALFPLANE, PSGPU_PRIM_NULL, -1 /* Instance */,
+        PSGPU_OP_UNION, PSGPU_OP_INTERSECT, PSGPU_OP_DIF, PSGPU_OP_SMOOTHDIF, PSGPU_OP_BLEND,
+        PSGPU_OP_RICCIBLEND, PSGPU_OP_GRADIENTBLEND, PSGPU_PRIM_FASTQPS, PSGPU_OP_PCM, PSGPU_OP_CACHE,
+        PSGPU_OP_WARPTWIST, PSGPU_OP_WARPTAPER, PSGPU_OP_WARPBEND, PSGPU_OP_WARPSHEAR, PSGPU_OP_TEXTURE};
+    return (t >= 0 && t < 29) ? map[t] : -1;
+}
+
+// PrepareBBoxes (PS_Polygonizer.cpp:55-309) with iso distance ISO_DIST + 5*MIN_CELL_SIZE.
+int psgpu_prepare_bboxes(float cellsize, PsSoaBlobPrims* P, PsSoaBoxMatrices* BM, PsSoaBlobOps* O) {
+    (void)cellsize;
+    if (!P || !O || P->ctPrims == 0 || P->ctPrims > 128) return PSGPU_RET_PARAM_ERROR;
+    const float iso = PSGPU_ISO_DIST + 5.0f * PSGPU_MIN_CELL_SIZE;
+    float* boxLo[3] = {P->vPrimBoxLoX, P->vPrimBoxLoY, P->vPrimBoxLoZ};
+    float* boxHi[3] = {P->vPrimBoxHiX, P->vPrimBoxHiY, P->vPrimBoxHiZ};
+    for (uint32_t i = 0; i < P->ctPrims; ++i) {
+        const float p[3] = {P->posX[i], P->posY[i], P->posZ[i]};
+        const float d[3] = {P->dirX[i], P->dirY[i], P->dirZ[i]};
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) { lo[a] = boxLo[a][i]; hi[a] = boxHi[a][i]; }
+        switch (P->skeletType[i]) {
+        case PSGPU_PRIM_POINT:
+            for (int a = 0; a < 3; ++a) { lo[a] = p[a] - iso; hi[a] = p[a] + iso; }
+            break;
+        case PSGPU_PRIM_LINE:
+            for (int a = 0; a < 3; ++a) {
+                const float e = iso * 1.0f + (3.0f * iso) * (d[a] - p[a]);
+                lo[a] = p[a] - e; hi[a] = d[a] + e;
+            }
+            break;
+        case PSGPU_PRIM_RING: case PSGPU_PRIM_DISC: {
+            const float r = P->resX[i] + iso;
+            for (int a = 0; a < 3; ++a) {
+                const float e = (r + iso) * (1.0f - d[a]) + iso * d[a];
+                lo[a] = p[a] - e; hi[a] = p[a] + e;
+            }
+        } break;
+        case PSGPU_PRIM_CYLINDER: {
+            const float r = P->resX[i], h = P->resY[i];
+            for (int a = 0; a < 3; ++a) {
+                const float s1 = p[a] + h * d[a];
+                const float e = (iso + r) * 1.0f + (0.5f * iso) * d[a];
+                lo[a] = p[a] - e; hi[a] = s1 + e;
+            }
+        } break;
+        case PSGPU_PRIM_CUBE: {
+            const float s = P->resX[i] + iso;
+            for (int a = 0; a < 3; ++a) { lo[a] = p[a] - s; hi[a] = p[a] + s; }
+        } break;
+        case PSGPU_PRIM_TRIANGLE: {
+            const float r[3] = {P->resX[i], P->resY[i], P->resZ[i]};
+            for (int a = 0; a < 3; ++a) {
+                float mn = p[a] < d[a] ? p[a] : d[a];
+                mn = mn < r[a] ? mn : r[a];
+                float mx = p[a] > d[a] ? p[a] : d[a];
+                mx = mx > r[a] ? mx : r[a];
+                lo[a] = mn - iso; hi[a] = mx + iso;
+            }
+        } break;
+        default: break;
+        }
+        const uint32_t im = P->idxMatrix[i];
+        if (im != 0 && BM && im < BM->count) {  // mat4Transform, PS_MATRIX4.h:199-209 (column vectors)
+            const float* M = &BM->matrix[im * PSGPU_BOX_MATRIX_STRIDE];
+            float tl[3], th[3];
+            for (int r = 0; r < 3; ++r) {
+                tl[r] = ((M[r] * lo[0] + M[4 + r] * lo[1]) + M[8 + r] * lo[2]) + M[12 + r];
+                th[r] = ((M[r] * hi[0] + M[4 + r] * hi[1]) + M[8 + r] * hi[2]) + M[12 + r];
+            }
+            memcpy(lo, tl, sizeof(lo));
+            memcpy(hi, th, sizeof(hi));
+        }
+        for (int a = 0; a < 3; ++a) { boxLo[a][i] = lo[a]; boxHi[a][i] = hi[a]; }
+        float* bl = &P->bboxLo.x;
+        float* bh = &P->bboxHi.x;
+        for (int a = 0; a < 3; ++a) {
+            if (i == 0) { bl[a] = lo[a]; bh[a] = hi[a]; }
+            else { bl[a] = bl[a] < lo[a] ? bl[a] : lo[a]; bh[a] = bh[a] > hi[a] ? bh[a] : hi[a]; }
+        }
+    }
+    if (O->ctOps > 0) {  // op boxes bottom-up (:238-307) as a post-order walk
+        std::vector<uint8_t> done(256, 0);
+        std::vector<uint32_t> st{0};
+        size_t guard = 0;
+        while (!st.empty()) {
+            if (++guard > 100000) return PSGPU_RET_INVALID_BVH;
+            const uint32_t op = st.back();
+            if (op >= 128) return PSGPU_RET_INVALID_BVH;
+            const uint32_t L = O->opLeftChild[op], R = O->opRightChild[op];
+            const int lop = (O->opChildKind[op] & 2) >> 1, rop = O->opChildKind[op] & 1;
+            if ((lop && !done[L]) || (rop && !done[R])) {
+                if (lop && !done[L]) st.push_back(L);
+                if (rop && !done[R]) st.push_back(R);
+                continue;
+            }
+            st.pop_back();
+            auto get = [&](int isOp, uint32_t k, float lo[3], float hi[3]) {
+                if (isOp) {
+                    lo[0] = O->vBoxLoX[k]; lo[1] = O->vBoxLoY[k]; lo[2] = O->vBoxLoZ[k];
+                    hi[0] = O->vBoxHiX[k]; hi[1] = O->vBoxHiY[k]; hi[2] = O->vBoxHiZ[k];
+                } else {
+                    for (int a = 0; a < 3; ++a) { lo[a] = boxLo[a][k]; hi[a] = boxHi[a][k]; }
+                }
+            };
+            float l0[3], h0[3], l1[3], h1[3];
+            get(lop, L, l0, h0);
+            get(rop, R, l1, h1);
+            float* oLo[3] = {O->vBoxLoX, O->vBoxLoY, O->vBoxLoZ};
+            float* oHi[3] = {O->vBoxHiX, O->vBoxHiY, O->vBoxHiZ};
+            for (int a = 0; a < 3; ++a) {
+                oLo[a][op] = l0[a] < l1[a] ? l0[a] : l1[a];
+                oHi[a][op] = h0[a] > h1[a] ? h0[a] : h1[a];
+            }
+            done[op] = 1;
+        }
+    }
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
+    if (!out) return PSGPU_RET_PARAM_ERROR;
+    *out = nullptr;
+    int n = psgpu_device_count();
+    if (deviceOrdinal < 0 || deviceOrdinal >= n) return PSGPU_RET_DEVICE_ERROR;
+    psgpu_ctx* c = new psgpu_ctx();
+    c->device = deviceOrdinal;
+    int rc = set_device(c);
+    if (rc != PSGPU_RET_SUCCESS) { delete c; return rc; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, deviceOrdinal) == hipSuccess && prop.multiProcessorCount > 0)
+        c->numCUs = prop.multiProcessorCount;
+    const CubeTables& T = cube_tables();
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        upload_tables(T.tri, T.ntri, T.corner1, T.axis) != hipSuccess ||
+        hipMalloc(&c->dModel, sizeof(DevModel)) != hipSuccess ||
+        hipMalloc(&c->ctr, sizeof(DevCounters)) != hipSuccess ||
+        hipMalloc(&c->dequeue, 4 * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc(&c->hostCtr, sizeof(DevCounters), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&c->initCtr, sizeof(DevCounters), hipHostMallocDefault) != hipSuccess) {
+        psgpu_destroy(c);
+        return PSGPU_RET_DEVICE_ERROR;
+    }
+    memset(c->initCtr, 0, sizeof(DevCounters));
+    c->initCtr->firstOverflow = 0x7fffffff;
+    for (int i = 0; i <= kNumKernels; ++i) (void)hipEventCreate(&c->ev[i]);
+    const char* cullEnv = getenv("PSGPU_CULL");
+    if (cullEnv) c->cull = atoi(cullEnv) != 0;
+    *out = c;
+    return PSGPU_RET_SUCCESS;
+}
+
+void psgpu_destroy(psgpu_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* bufs[] = {c->dModel, c->passMask, c->passList, c->counts, c->voff, c->toff, c->vq, c->tq,
+                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->dequeue};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->hostCtr) (void)hipHostFree(c->hostCtr);
+    if (c->initCtr) (void)hipHostFree(c->initCtr);
+    for (int i = 0; i <= kNumKernels; ++i)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
+    if (!c) return PSGPU_RET_PARAM_ERROR;
+    if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
+    else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
+    else return PSGPU_RET_PARAM_ERROR;
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats,
+                    const PsSoaBlobOps* ops) {
+    if (!c || !prims || !mats || !ops) return PSGPU_RET_PARAM_ERROR;
+    int rc = set_device(c);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    DevModel* m = new DevModel;
+    rc = build_device_model(*prims, *mats, *ops, *m);
+    if (rc != PSGPU_RET_SUCCESS) { delete m; return rc; }
+    if (c->pending) (void)hipStreamSynchronize(c->runStream);
+    c->model = *m;
+    delete m;
+    memcpy(&c->primsHost, prims, sizeof(PsSoaBlobPrims));
+    PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
+    PSGPU_CHECK(hipStreamSynchronize(c->stream));
+    c->haveModel = true;
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t mpuEnd, void* stream) {
+    if (!c || !c->haveModel) return PSGPU_RET_PARAM_ERROR;
+    if (c->primsHost.ctPrims == 0 || !(cellsize > 0.0f)) return PSGPU_RET_PARAM_ERROR;
+    int rc = set_device(c);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (c->pending && c->runStream != s) (void)hipStreamSynchronize(c->runStream);
+    c->cs = cellsize;
+    lattice_dims(cellsize, c->primsHost.bboxLo, c->primsHost.bboxHi, c->dims);
+    const uint64_t total = (uint64_t)c->dims[0] * c->dims[1] * c->dims[2];
+    if (total > 0xffffffffull) return PSGPU_RET_PARAM_ERROR;
+    const uint32_t end = (uint32_t)std::min<uint64_t>(mpuEnd, total);
+    c->mpuBegin = std::min(mpuBegin, end);
+    c->mpuCount = end - c->mpuBegin;
+    rc = ensure_buffers(c, c->mpuCount);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    rc = enqueue(c, s);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    c->runStream = s;
+    c->pending = true;
+    c->haveResult = false;
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
+    if (!c) return PSGPU_RET_PARAM_ERROR;
+    if (c->pending) {
+        int rc = set_device(c);
+        if (rc != PSGPU_RET_SUCCESS) return rc;
+        PSGPU_CHECK(hipStreamSynchronize(c->runStream));
+        c->pending = false;
+        // grow and re-run if the compact outputs did not fit
+        for (int attempt = 0; attempt < 4; ++attempt) {
+            const DevCounters h = *c->hostCtr;
+            if (h.vCount <= c->vcap && h.tCount <= c->tcap) break;
+            c->vcap = std::max(c->vcap, h.vCount + h.vCount / 8 + 1024);
+            c->tcap = std::max(c->tcap, h.tCount + h.tCount / 8 + 1024);
+            rc = ensure_buffers(c, c->mpuCount);
+            if (rc != PSGPU_RET_SUCCESS) return rc;
+            rc = enqueue(c, c->runStream);
+            if (rc != PSGPU_RET_SUCCESS) return rc;
+            PSGPU_CHECK(hipStreamSynchronize(c->runStream));
+        }
+        if (c->timing && c->mpuCount > 0) {
+            for (int k = 0; k < kNumKernels; ++k) {
+                float ms = 0.0f;
+                if (hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]) == hipSuccess) c->lastMs[k] = ms;
+            }
+        }
+        const DevCounters h = *c->hostCtr;
+        PsMeshInfo& I = c->info;
+        memset(&I, 0, sizeof(I));
+        I.ctMPUs = c->mpuCount;
+        I.ctPassedPrecheck = c->mpuCount ? h.passCount : 0;
+        I.ctSurfaceMPUs = c->mpuCount ? h.surfaceCount : 0;
+        I.ctVertices = c->mpuCount ? h.vCount : 0;
+        I.ctTriangles = c->mpuCount ? h.tCount : 0;
+        I.firstOverflowMPU = (c->mpuCount && h.firstOverflow != 0x7fffffff) ? h.firstOverflow : -1;
+        I.ctLaneEvals = 8ull * c->mpuCount + 512ull * I.ctPassedPrecheck + 8ull * I.ctVertices;
+        c->haveResult = true;
+    }
+    if (!c->haveResult) return PSGPU_RET_PARAM_ERROR;
+    if (info) *info = c->info;
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_last_kernel_times(psgpu_ctx* c, float* ms, int maxKernels, const char** names) {
+    if (!c) return 0;
+    int n = std::min(maxKernels, kNumKernels);
+    for (int k = 0; k < n; ++k) {
+        if (ms) ms[k] = c->lastMs[k];
+        if (names) names[k] = kKernelNames[k];
+    }
+    return n;
+}
+
+int psgpu_mesh_device(psgpu_ctx* c, PsMeshDevice* out) {
+    if (!c || !out) return PSGPU_RET_PARAM_ERROR;
+    int rc = psgpu_finish(c, nullptr);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    out->pos = c->pos;
+    out->nrm = c->nrm;
+    out->col = c->col;
+    out->tris = c->tris;
+    out->surfaceMpuIds = c->passList;
+    out->mpuVertexOffset = c->voff;
+    out->mpuTriangleOffset = c->toff;
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_download_mesh(psgpu_ctx* c, float* pos, float* nrm, float* col, uint32_t* tris, uint32_t* ids,
+                        uint32_t* voff, uint32_t* toff) {
+    PsMeshInfo I;
+    int rc = psgpu_finish(c, &I);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    const size_t V = I.ctVertices, T = I.ctTriangles, W = I.ctPassedPrecheck;
+    if (pos && V) PSGPU_CHECK(hipMemcpy(pos, c->pos, V * 12, hipMemcpyDeviceToHost));
+    if (nrm && V) PSGPU_CHECK(hipMemcpy(nrm, c->nrm, V * 12, hipMemcpyDeviceToHost));
+    if (col && V) PSGPU_CHECK(hipMemcpy(col, c->col, V * 12, hipMemcpyDeviceToHost));
+    if (tris && T) PSGPU_CHECK(hipMemcpy(tris, c->tris, T * 12, hipMemcpyDeviceToHost));
+    if (ids && W) PSGPU_CHECK(hipMemcpy(ids, c->passList, W * 4, hipMemcpyDeviceToHost));
+    if (voff) {
+        if (W) PSGPU_CHECK(hipMemcpy(voff, c->voff, (W + 1) * 4, hipMemcpyDeviceToHost));
+        else voff[0] = 0;
+    }
+    if (toff) {
+        if (W) PSGPU_CHECK(hipMemcpy(toff, c->toff, (W + 1) * 4, hipMemcpyDeviceToHost));
+        else toff[0] = 0;
+    }
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_download_stats(psgpu_ctx* c, PsMpuStats* stats) {
+    PsMeshInfo I;
+    int rc = psgpu_finish(c, &I);
+    if (rc != PSGPU_RET_SUCCESS || !stats) return rc == PSGPU_RET_SUCCESS ? PSGPU_RET_PARAM_ERROR : rc;
+    const uint32_t W = I.ctPassedPrecheck;
+    std::vector<uint32_t> ids(W), cnt(2 * (size_t)W);
+    if (W) {
+        PSGPU_CHECK(hipMemcpy(ids.data(), c->passList, W * 4, hipMemcpyDeviceToHost));
+        PSGPU_CHECK(hipMemcpy(cnt.data(), c->counts, (size_t)W * 8, hipMemcpyDeviceToHost));
+    }
+    memset(stats, 0, sizeof(PsMpuStats) * c->mpuCount);
+    for (uint32_t w = 0; w < W; ++w) {
+        PsMpuStats& s = stats[ids[w] - c->mpuBegin];
+        s.passedPrecheck = 1;
+        s.ctFieldEvals = 128;
+        s.ctVertices = cnt[2 * w];
+        s.ctTriangles = cnt[2 * w + 1];
+    }
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt) {
+    PsMeshInfo I;
+    int rc = psgpu_finish(c, &I);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (outCt) *outCt = c->mpuCount;
+    if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
+    if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
+    if (!mpus) return PSGPU_RET_PARAM_ERROR;
+    const size_t V = I.ctVertices, T = I.ctTriangles, W = I.ctPassedPrecheck;
+    std::vector<float> pos(V * 3), nrm(V * 3), col(V * 3);
+    std::vector<uint32_t> tris(T * 3), ids(W), voff(W + 1), toff(W + 1);
+    rc = psgpu_download_mesh(c, pos.data(), nrm.data(), col.data(), tris.data(), ids.data(), voff.data(), toff.data());
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
+    for (uint32_t l = 0; l < c->mpuCount; ++l) {  // Polygonize :360-371
+        const uint32_t m = c->mpuBegin + l;
+        const uint32_t k = m % c->dims[2], j = (m / c->dims[2]) % c->dims[1], i = m / (c->dims[2] * c->dims[1]);
+        PsMPU& M = mpus[l];
+        M.bboxLo.x = c->primsHost.bboxLo.x + (float)i * side;
+        M.bboxLo.y = c->primsHost.bboxLo.y + (float)j * side;
+        M.bboxLo.z = c->primsHost.bboxLo.z + (float)k * side;
+        M.ctVertices = 0;
+        M.ctTriangles = 0;
+        M.ctFieldEvals = 0;
+    }
+    for (size_t w = 0; w < W; ++w) {
+        PsMPU& M = mpus[ids[w] - c->mpuBegin];
+        const uint32_t v0 = voff[w], nv = voff[w + 1] - v0;
+        const uint32_t t0 = toff[w], nt = toff[w + 1] - t0;
+        M.ctFieldEvals = 128;
+        M.ctVertices = (uint16_t)nv;
+        M.ctTriangles = (uint16_t)nt;
+        memcpy(M.vPos, &pos[(size_t)v0 * 3], (size_t)nv * 12);
+        memcpy(M.vNorm, &nrm[(size_t)v0 * 3], (size_t)nv * 12);
+        memcpy(M.vColor, &col[(size_t)v0 * 3], (size_t)nv * 12);
+        for (uint32_t t = 0; t < nt * 3; ++t) M.triangles[t] = (uint16_t)(tris[(size_t)t0 * 3 + t] - v0);
+    }
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats,
+                          const PsSoaBlobOps* ops, PsMPU* mpus, uint32_t capacity, uint32_t* outCt,
+                          PsMpuStats* stats) {
+    if (!c || !prims) return PSGPU_RET_PARAM_ERROR;
+    if (prims->ctPrims == 0) return PSGPU_RET_PARAM_ERROR;  // Polygonize :322-323
+    int rc = psgpu_set_model(c, prims, mats, ops);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    rc = psgpu_polygonize(c, cellsize, 0, 0xffffffffu, nullptr);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    rc = psgpu_export_polympus(c, mpus, capacity, outCt);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (stats) rc = psgpu_download_stats(c, stats);
+    return rc;
+}
+
+// Field probe (FieldComputer::fieldValue / fieldValueAndColor on arbitrary points).
+// mode 0: 4-lane groups (consecutive points), 1: per point, 2: per point + colour.
+int psgpu_field_values(psgpu_ctx* c, const float* xyz, uint32_t n, int mode, float* out, float* colOut) {
+    if (!c || !c->haveModel || !xyz || !out || mode < 0 || mode > 2) return PSGPU_RET_PARAM_ERROR;
+    int rc = set_device(c);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (n == 0) return PSGPU_RET_SUCCESS;
+    float *dx = nullptr, *dout = nullptr, *dcol = nullptr;
+    PSGPU_CHECK(hipMalloc(&dx, (size_t)n * 12));
+    PSGPU_CHECK(hipMalloc(&dout, (size_t)n * 4));
+    PSGPU_CHECK(hipMalloc(&dcol, (size_t)n * 12));
+    PSGPU_CHECK(hipMemcpy(dx, xyz, (size_t)n * 12, hipMemcpyHostToDevice));
+    Params p = make_params(c);
+    hipError_t e = launch_probe(p, c->stream, dx, dout, dcol, n, mode);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && colOut) e = hipMemcpy(colOut, dcol, (size_t)n * 12, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    (void)hipFree(dout);
+    (void)hipFree(dcol);
+    return hip_fail(e, "psgpu_field_values");
+}
+
+}  // extern "C"

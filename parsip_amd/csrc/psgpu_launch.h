@@ -1,0 +1,25 @@
+// psgpu_launch.h — host entry points of the kernels in psgpu_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "psgpu_model.h"
+
+namespace psgpu {
+
+hipError_t upload_tables(const int8_t tri[256][16], const uint8_t ntri[256], const uint8_t corner1[12],
+                         const uint8_t axis[12]);
+size_t mpu_lds_bytes(uint32_t slots);
+size_t walk_lds_bytes(uint32_t slots);
+size_t precheck_lds_bytes(uint32_t slots);
+hipError_t launch_precheck(const Params& p, hipStream_t s);
+hipError_t launch_compact(const Params& p, hipStream_t s);
+hipError_t launch_mpu(const Params& p, hipStream_t s);
+hipError_t launch_scan(const Params& p, hipStream_t s);
+hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks);
+hipError_t launch_tris(const Params& p, hipStream_t s, uint32_t blocks);
+hipError_t launch_probe(const Params& p, hipStream_t s, const float* xyz, float* out, float* col, uint32_t n,
+                        int mode);
+
+}  // namespace psgpu

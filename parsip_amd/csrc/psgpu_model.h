@@ -1,0 +1,127 @@
+// psgpu_model.h — device-side image of a linearised BlobTree (host + device).
+//
+// The reference walks the op tree per SIMD call with an explicit stack
+// (FieldComputer::fieldValue, PS_Polygonizer.cpp:1184-1376).  On CDNA4 every
+// wavefront walks the same tree, so the host flattens the walk once per model into
+// a short wave-uniform program (read with scalar loads) and the per-lane state is
+// reduced to a resume pc (op-box pruning) plus a small value stack in LDS.
+//
+//   ENTER  op, skipTo, out   depth>3 op-box test (PS_Polygonizer.cpp:1228-1252);
+//                            lanes whose 4-lane group is outside resume at skipTo
+//                            with field 0 in slot `out`.
+//   PRIM   prim, out         computePrimitiveField (:934-1179) into slot `out`.
+//   OP     op, type, l, r    binary combine (:1282-1338) into slot `out`.
+//   SUMPRIM prim             no-op trees: running sum of all prims (:1356-1368).
+//
+// The program order is the reference's processing order (post-order, right child
+// first, :1344-1352), which also fixes the "stale outField" semantics of op types
+// that have no case in the reference switch.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace psgpu {
+
+enum InstrKind : uint8_t { kEnter = 0, kPrim = 1, kOp = 2, kSumPrim = 3 };
+
+struct Instr {           // 16 B, one s_load_dwordx4
+    uint8_t kind;
+    uint8_t type;        // OP: op type (PS_Polygonizer.h enum)
+    uint8_t out;         // value slot written
+    uint8_t lslot;       // OP: slot of left child value
+    uint8_t rslot;       // OP: slot of right child value
+    uint8_t childKind;   // OP: bit1 left is op, bit0 right is op
+    uint8_t L, R;        // OP: child indices (prim or op ids)
+    uint16_t idx;        // ENTER/OP: op id; PRIM/SUMPRIM: prim id
+    uint16_t skipTo;     // ENTER: pc after the op's OP instruction
+    uint32_t pad;
+};
+static_assert(sizeof(Instr) == 16, "Instr size");
+
+struct DevOp {           // 32 B
+    float lo[3];
+    float hi[3];
+    float resY;          // RicciBlend exponent (SOABlobOps::resY)
+    uint32_t type;
+};
+static_assert(sizeof(DevOp) == 32, "DevOp size");
+
+struct DevPrim {         // 128 B
+    float pos[3];
+    float dir[3];
+    float res[3];
+    float col[3];
+    uint32_t type;
+    uint32_t hasMatrix;  // idxMatrix != 0
+    uint32_t cullable;   // exact culling bound valid for this prim (see kernels)
+    float cullRadius;    // support radius used by the cull test
+    float mat[12];       // SOABlobPrimMatrices row-major 3x4 (12-float stride)
+    float pad[4];
+};
+static_assert(sizeof(DevPrim) == 128, "DevPrim size");
+
+constexpr int kMaxInstr = 512;
+constexpr int kMaxSlots = 64;
+
+struct DevModel {
+    uint32_t nInstr;
+    uint32_t nSlots;
+    uint32_t ctPrims;
+    uint32_t ctOps;
+    uint32_t pad[4];
+    Instr instr[kMaxInstr];
+    DevOp ops[128];
+    DevPrim prims[128];
+};
+
+// Compact-mesh work records written by the MPU kernel.
+struct VertexRec {       // 8 B: surface-MPU slot, local vertex id, edge key
+    uint32_t w;
+    uint32_t vidKey;     // vid | key << 16, key = sx | sy<<3 | sz<<6 | axis<<9
+};
+struct TriRec {          // 16 B
+    uint32_t w;
+    uint32_t tlocal;
+    uint32_t v01;        // v0 | v1 << 16
+    uint32_t v2;
+};
+
+// Device-side scalars of one polygonization.
+struct DevCounters {
+    uint32_t passCount;      // MPUs that passed S1
+    uint32_t vCount;         // vertices reserved
+    uint32_t tCount;         // triangles reserved
+    uint32_t surfaceCount;   // MPUs with >= 1 triangle
+    int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
+    uint32_t pad[3];
+};
+
+// Kernel arguments of one polygonization (one struct, passed by value).
+struct Params {
+    const DevModel* __restrict__ model;
+    float cs;           // cellsize
+    float side;         // cellsize * 7.0f (MPU side)
+    float lo[3];        // scene bboxLo
+    uint32_t dims[3];   // MPU lattice
+    uint32_t mpuBegin;
+    uint32_t mpuCount;
+    uint32_t cull;      // exact per-wave primitive culling enabled
+    uint32_t* passMask;     // ceil(mpuCount/32)
+    uint32_t* passList;     // mpuCount, global MPU ids
+    uint2* counts;          // mpuCount, (V,T) per passing slot
+    uint32_t* voff;         // mpuCount + 1
+    uint32_t* toff;         // mpuCount + 1
+    VertexRec* vq;
+    uint32_t vcap;
+    TriRec* tq;
+    uint32_t tcap;
+    float* pos;
+    float* nrm;
+    float* col;
+    uint32_t* tris;
+    DevCounters* ctr;
+    uint32_t* dequeue;      // [2] work counters for k_vertex / k_tris
+    uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
+};
+
+}  // namespace psgpu

@@ -1,0 +1,263 @@
+"""ctypes binding of the C-ABI library (include/parsip_gpu.h) and the host-side mirror of
+the reference's polygonizer interface.
+
+Reference interface mirrored (Parsip100/PS_SimdPoly/include/PS_Polygonizer.h:384-393):
+
+    U32 CountMPUNeeded(float cellsize, const svec3f& lo, const svec3f& hi);
+    int PrepareBBoxes(float cellsize, SOABlobPrims&, SOABlobBoxMatrices&, SOABlobOps&);
+    int Polygonize(float cellsize, const SOABlobPrims&, const SOABlobPrimMatrices&,
+                   const SOABlobOps&, PolyMPUs&, MPUSTATS* = NULL);
+
+``Polygonize`` returns the reference's codes (1 success, -1 parameter error) plus the
+library's explicit -3..-6 (invalid tree, MPU capacity, per-MPU capacity, device error).
+There is no CPU fallback: if the HIP library or a GPU is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import soa
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libparsip_gpu.so")
+
+
+class PsMeshInfo(ctypes.Structure):
+    _fields_ = [("ctMPUs", ctypes.c_uint32), ("ctPassedPrecheck", ctypes.c_uint32),
+                ("ctSurfaceMPUs", ctypes.c_uint32), ("ctVertices", ctypes.c_uint32),
+                ("ctTriangles", ctypes.c_uint32), ("firstOverflowMPU", ctypes.c_int32),
+                ("ctLaneEvals", ctypes.c_uint64)]
+
+
+class PsMeshDevice(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "nrm", "col", "tris", "surfaceMpuIds",
+                                               "mpuVertexOffset", "mpuTriangleOffset")]
+
+
+EXPORTED_SYMBOLS = [
+    "psgpu_count_mpus", "psgpu_mpu_dims", "psgpu_prepare_bboxes", "psgpu_translate_blobtree_type",
+    "psgpu_tritable", "psgpu_version", "psgpu_create", "psgpu_destroy", "psgpu_device_count",
+    "psgpu_set_model", "psgpu_polygonize", "psgpu_finish", "psgpu_mesh_device", "psgpu_download_mesh",
+    "psgpu_download_stats", "psgpu_export_polympus", "psgpu_polygonize_mpus", "psgpu_last_kernel_times",
+    "psgpu_field_values", "psgpu_set_option",
+]
+
+
+def load(build_if_missing: bool = True):
+    """Load libparsip_gpu.so (building it in-tree with hipcc if absent)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH) and build_if_missing:
+        from .build import build
+        build()
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, i32, f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
+    sig = {
+        "psgpu_count_mpus": ([f32, vp, vp], u32),
+        "psgpu_mpu_dims": ([f32, vp, vp], i32),
+        "psgpu_prepare_bboxes": ([f32, vp, vp, vp], i32),
+        "psgpu_translate_blobtree_type": ([i32], i32),
+        "psgpu_tritable": ([vp], None),
+        "psgpu_version": ([], ctypes.c_char_p),
+        "psgpu_create": ([i32, ctypes.POINTER(vp)], i32),
+        "psgpu_destroy": ([vp], None),
+        "psgpu_device_count": ([], i32),
+        "psgpu_set_model": ([vp, vp, vp, vp], i32),
+        "psgpu_polygonize": ([vp, f32, u32, u32, vp], i32),
+        "psgpu_finish": ([vp, ctypes.POINTER(PsMeshInfo)], i32),
+        "psgpu_mesh_device": ([vp, ctypes.POINTER(PsMeshDevice)], i32),
+        "psgpu_download_mesh": ([vp, vp, vp, vp, vp, vp, vp, vp], i32),
+        "psgpu_download_stats": ([vp, vp], i32),
+        "psgpu_export_polympus": ([vp, vp, u32, ctypes.POINTER(u32)], i32),
+        "psgpu_polygonize_mpus": ([vp, f32, vp, vp, vp, vp, u32, ctypes.POINTER(u32), vp], i32),
+        "psgpu_last_kernel_times": ([vp, vp, i32, vp], i32),
+        "psgpu_field_values": ([vp, vp, u32, i32, vp, vp], i32),
+        "psgpu_set_option": ([vp, i32, ctypes.c_int64], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _LIB = L
+    return L
+
+
+class PsgpuError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with code {code}")
+        self.code = code
+
+
+def _check(rc: int, what: str) -> int:
+    if rc != soa.RET_SUCCESS:
+        raise PsgpuError(rc, what)
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# host-only helpers (no GPU needed)
+def count_mpus(cellsize: float, lo, hi) -> int:
+    """CountMPUNeeded (PS_Polygonizer.cpp:388-412)."""
+    lo = np.ascontiguousarray(lo, np.float32)
+    hi = np.ascontiguousarray(hi, np.float32)
+    return int(load().psgpu_count_mpus(cellsize, lo.ctypes.data, hi.ctypes.data))
+
+
+def prepare_bboxes(cellsize: float, model: soa.Model) -> int:
+    """PrepareBBoxes (PS_Polygonizer.cpp:55-309), in place on the model's SoA."""
+    return load().psgpu_prepare_bboxes(cellsize, model.prims.ctypes.data, model.boxmats.ctypes.data,
+                                       model.ops.ctypes.data)
+
+
+def tritable() -> np.ndarray:
+    t = np.zeros((256, 16), np.int32)
+    load().psgpu_tritable(t.ctypes.data)
+    return t
+
+
+def device_count() -> int:
+    return int(load().psgpu_device_count())
+
+
+@dataclass
+class Mesh:
+    """Compact mesh in the reference's MPU order (concatenation of vMPUs[i] arrays)."""
+
+    pos: np.ndarray            # (V,3) f32
+    nrm: np.ndarray            # (V,3) f32
+    col: np.ndarray            # (V,3) f32
+    tris: np.ndarray           # (T,3) u32 global vertex ids
+    surface_mpus: np.ndarray   # (W,) u32 global MPU id of every S1 survivor, ascending
+    vertex_offsets: np.ndarray  # (W+1,)
+    triangle_offsets: np.ndarray  # (W+1,)
+
+    def local_tris(self) -> np.ndarray:
+        """Triangles with MPU-local (U16) ids, as stored in MPU::triangles."""
+        per = np.repeat(self.vertex_offsets[:-1].astype(np.int64),
+                        np.diff(self.triangle_offsets).astype(np.int64))
+        return (self.tris.astype(np.int64) - per[:, None]).astype(np.uint16)
+
+
+class Polygonizer:
+    """One device context: a model in HBM and the buffers of the last polygonization."""
+
+    def __init__(self, device: int = 0):
+        L = load()
+        if L.psgpu_device_count() <= device:
+            raise PsgpuError(soa.RET_DEVICE_ERROR, f"no HIP device {device}")
+        self._ctx = ctypes.c_void_p()
+        _check(L.psgpu_create(device, ctypes.byref(self._ctx)), "psgpu_create")
+        self._L = L
+        self.model = None
+        self.info = None
+
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._L.psgpu_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    __del__ = close
+
+    def set_option(self, option: int, value: int) -> None:
+        _check(self._L.psgpu_set_option(self._ctx, option, value), "psgpu_set_option")
+
+    def set_model(self, model: soa.Model) -> None:
+        p, m, o = model.ptrs()
+        _check(self._L.psgpu_set_model(self._ctx, p, m, o), "psgpu_set_model")
+        self.model = model
+
+    def polygonize(self, cellsize: float, mpu_begin: int = 0, mpu_end: int | None = None,
+                   stream: int | None = None) -> None:
+        """Enqueue (async).  ``stream`` is a raw hipStream_t handle or None."""
+        end = 0xFFFFFFFF if mpu_end is None else mpu_end
+        _check(self._L.psgpu_polygonize(self._ctx, cellsize, mpu_begin, end, stream), "psgpu_polygonize")
+
+    def finish(self) -> PsMeshInfo:
+        info = PsMeshInfo()
+        _check(self._L.psgpu_finish(self._ctx, ctypes.byref(info)), "psgpu_finish")
+        self.info = info
+        return info
+
+    def run(self, cellsize: float, mpu_begin: int = 0, mpu_end: int | None = None) -> PsMeshInfo:
+        self.polygonize(cellsize, mpu_begin, mpu_end)
+        return self.finish()
+
+    def download(self) -> Mesh:
+        info = self.finish()
+        V, T, W = info.ctVertices, info.ctTriangles, info.ctPassedPrecheck
+        pos = np.zeros((V, 3), np.float32)
+        nrm = np.zeros((V, 3), np.float32)
+        col = np.zeros((V, 3), np.float32)
+        tris = np.zeros((T, 3), np.uint32)
+        ids = np.zeros(W, np.uint32)
+        voff = np.zeros(W + 1, np.uint32)
+        toff = np.zeros(W + 1, np.uint32)
+        _check(self._L.psgpu_download_mesh(self._ctx, pos.ctypes.data, nrm.ctypes.data, col.ctypes.data,
+                                           tris.ctypes.data, ids.ctypes.data, voff.ctypes.data,
+                                           toff.ctypes.data), "psgpu_download_mesh")
+        return Mesh(pos, nrm, col, tris, ids, voff, toff)
+
+    def stats(self) -> np.ndarray:
+        info = self.finish()
+        st = np.zeros(info.ctMPUs, soa.MPU_STATS_DTYPE)
+        _check(self._L.psgpu_download_stats(self._ctx, st.ctypes.data), "psgpu_download_stats")
+        return st
+
+    def export_polympus(self, capacity: int | None = None) -> np.ndarray:
+        info = self.finish()
+        cap = info.ctMPUs if capacity is None else capacity
+        out = np.zeros(max(cap, 1), soa.MPU_DTYPE)
+        ct = ctypes.c_uint32()
+        _check(self._L.psgpu_export_polympus(self._ctx, out.ctypes.data, cap, ctypes.byref(ct)),
+               "psgpu_export_polympus")
+        return out[:ct.value]
+
+    def device_mesh(self) -> PsMeshDevice:
+        d = PsMeshDevice()
+        _check(self._L.psgpu_mesh_device(self._ctx, ctypes.byref(d)), "psgpu_mesh_device")
+        return d
+
+    def kernel_times(self) -> dict:
+        ms = (ctypes.c_float * 8)()
+        names = (ctypes.c_char_p * 8)()
+        n = self._L.psgpu_last_kernel_times(self._ctx, ms, 8, names)
+        return {names[i].decode(): ms[i] for i in range(n)}
+
+    def field_values(self, xyz: np.ndarray, mode: int = 0):
+        """mode 0: quads of consecutive points; 1: per point; 2: per point + colour."""
+        xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        n = len(xyz)
+        out = np.zeros(n, np.float32)
+        col = np.zeros((n, 3), np.float32)
+        _check(self._L.psgpu_field_values(self._ctx, xyz.ctypes.data, n, mode, out.ctypes.data, col.ctypes.data),
+               "psgpu_field_values")
+        return (out, col) if mode == 2 else out
+
+
+_DEFAULT = {}
+
+
+def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None = None, device: int = 0,
+               stats: np.ndarray | None = None):
+    """Blocking drop-in for PS::SIMDPOLY::Polygonize.
+
+    Fills ``poly_mpus`` (a MPU_DTYPE array, default capacity MAX_MPU_COUNT as in PolyMPUs)
+    and returns ``(code, ctMPUs, poly_mpus)``.
+    """
+    if model.ct_prims == 0:
+        return soa.RET_PARAM_ERROR, 0, poly_mpus
+    if device not in _DEFAULT:
+        _DEFAULT[device] = Polygonizer(device)
+    ctx = _DEFAULT[device]
+    if poly_mpus is None:
+        poly_mpus = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
+    ct = ctypes.c_uint32()
+    p, m, o = model.ptrs()
+    rc = ctx._L.psgpu_polygonize_mpus(ctx._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
+                                      ctypes.byref(ct), None if stats is None else stats.ctypes.data)
+    return rc, ct.value, poly_mpus

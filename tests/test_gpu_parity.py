@@ -1,0 +1,138 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
+
+Bar (north_star): MPU lattice, S1/S2 decisions, per-MPU vertex and
+triangle counts, vertex order and triangle indices bit-exact; positions bit-exact
+(north_star allows 1e-5); normals and colours bit-exact against the oracle's IEEE
+1/sqrt (the reference's _mm_rsqrt_ps is CPU-vendor specific: see test_oracle.py for
+the 2e-3 normal tolerance against that variant).
+"""
+import numpy as np
+import pytest
+
+from parity_util import assert_bits_equal, assert_mesh_matches
+from parsip_amd import gpu, soa, synth
+from parsip_amd.soa import NodeType
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1):
+    poly.set_option(2, cull)
+    poly.set_model(model)
+    poly.run(cs, begin, end)
+    gm = poly.download()
+    gs = poly.stats()
+    om = oracle.polygonize(model, cs, begin, 0xFFFFFFFF if end is None else end, threads=8)
+    return gm, gs, om
+
+
+@pytest.mark.parametrize("name", ["C1", "C2"])
+@pytest.mark.parametrize("cull", [0, 1])
+def test_configs_bit_exact(gpu_poly, oracle, name, cull):
+    model, cs, _ = synth.make_config(name)
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs, cull=cull)
+    assert len(gm.pos) > 0
+    assert_mesh_matches(gm, gs, om)
+
+
+def test_c1_reference_counts(gpu_poly):
+    """C1 is PRNG-independent; SURVEY.md §6/§8(d) record the reference's own output for it
+    (the survey compiled PS_Polygonizer.cpp): 125 MPUs, 109 past S1, 1,326 V, 2,024 T."""
+    model, cs, _ = synth.make_config("C1")
+    gpu_poly.set_model(model)
+    info = gpu_poly.run(cs)
+    assert (info.ctMPUs, info.ctPassedPrecheck, info.ctVertices, info.ctTriangles) == (125, 109, 1326, 2024)
+
+
+def test_c3_full_size(gpu_poly, oracle):
+    """Headline workload (256^3, 32 prims, pruning live) against the oracle, in full."""
+    model, cs, _ = synth.make_config("C3")
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert_mesh_matches(gm, gs, om)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_trees(gpu_poly, oracle, seed):
+    ops = [NodeType.BLEND, NodeType.UNION, NodeType.INTERSECT, NodeType.DIF, NodeType.SMOOTHDIF,
+           NodeType.RICCIBLEND, NodeType.WARPTWIST, NodeType.GRADIENTBLEND]
+    model = synth.random_model(seed, n_prims=3 + 3 * seed, op_types=ops, matrices=seed % 2 == 1)
+    cs = float(np.float32(4.0 / 48))
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert_mesh_matches(gm, gs, om)
+
+
+def test_disc_ring_triangle_null(gpu_poly, oracle):
+    """Every primitive switch case incl. rsqrt users and the no-case default."""
+    types = [NodeType.DISC, NodeType.RING, NodeType.POINT, NodeType.TRIANGLE, NodeType.CUBE]
+    model = synth.random_model(11, n_prims=10, types=types)
+    cs = float(np.float32(4.0 / 40))
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert_mesh_matches(gm, gs, om)
+
+
+def test_mpu_range_partition(gpu_poly, oracle):
+    """Contiguous MPU ranges (the multi-GPU split) concatenate to the full result."""
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+    gpu_poly.run(cs)
+    full = gpu_poly.download()
+    n = gpu_poly.finish().ctMPUs
+    cuts = [0, n // 3, n // 2 + 17, n]
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        gpu_poly.run(cs, a, b)
+        parts.append(gpu_poly.download())
+    pos = np.concatenate([p.pos for p in parts])
+    assert_bits_equal(pos, full.pos, "partitioned positions")
+    lt = np.concatenate([p.local_tris() for p in parts])
+    np.testing.assert_array_equal(lt, full.local_tris())
+    om = oracle.polygonize(model, cs, cuts[1], cuts[2], threads=8)
+    gpu_poly.run(cs, cuts[1], cuts[2])
+    assert_mesh_matches(gpu_poly.download(), gpu_poly.stats(), om)
+
+
+def test_field_probe_quads(gpu_poly, oracle):
+    model, cs, _ = synth.make_config("C3")
+    gpu_poly.set_model(model)
+    rng = np.random.default_rng(3)
+    # quads of 4 z-consecutive points like S2, plus scattered quads
+    base = rng.uniform(-4, 4, (4096, 3)).astype(np.float32)
+    pts = np.repeat(base, 4, axis=0)
+    pts[:, 2] += np.tile(np.arange(4, dtype=np.float32) * np.float32(1 / 32), 4096)
+    g = gpu_poly.field_values(pts, mode=0)
+    o = oracle.field_value(model, pts[:, 0], pts[:, 1], pts[:, 2])
+    assert_bits_equal(g, o, "fieldValue (4-lane groups)")
+
+
+def test_field_probe_colour(gpu_poly, oracle):
+    model, cs, _ = synth.make_config("C3")
+    gpu_poly.set_model(model)
+    rng = np.random.default_rng(5)
+    pts = rng.uniform(-3, 3, (2048, 3)).astype(np.float32)
+    f, c = gpu_poly.field_values(pts, mode=2)
+    rep = np.repeat(pts, 4, axis=0)
+    of, oc = oracle.field_value_and_color(model, rep[:, 0], rep[:, 1], rep[:, 2])
+    assert_bits_equal(f, of[::4], "fieldValueAndColor field")
+    assert_bits_equal(c, oc[::4], "fieldValueAndColor colour")
+
+
+def test_drop_in_polygonize(gpu_poly, oracle):
+    """psgpu_polygonize_mpus fills the reference PolyMPUs layout (21,524-B MPUs)."""
+    model, cs, _ = synth.make_config("C2")
+    rc, ct, mpus = gpu.Polygonize(cs, model)
+    assert rc == soa.RET_SUCCESS and ct == 6859
+    om = oracle.polygonize(model, cs, threads=8)
+    np.testing.assert_array_equal(mpus["ctVertices"][:ct], om.stats[:, 2])
+    np.testing.assert_array_equal(mpus["ctTriangles"][:ct], om.stats[:, 3])
+    np.testing.assert_array_equal(mpus["ctFieldEvals"][:ct], om.stats[:, 1])
+    origins = soa.mpu_origins(cs, *model.bbox)
+    assert_bits_equal(mpus["bboxLo"][:ct], origins, "MPU origins")
+    voff = om.vertex_offsets
+    toff = om.triangle_offsets
+    for i in np.flatnonzero(om.stats[:, 2])[:200]:
+        nv, nt = om.stats[i, 2], om.stats[i, 3]
+        assert_bits_equal(mpus["vPos"][i, :nv * 3].reshape(-1, 3), om.pos[voff[i]:voff[i] + nv], "vPos")
+        np.testing.assert_array_equal(mpus["triangles"][i, :nt * 3].reshape(-1, 3), om.tris[toff[i]:toff[i] + nt])
+    # reference error code for an empty model
+    empty = soa.Model.empty()
+    assert gpu.Polygonize(cs, empty)[0] == soa.RET_PARAM_ERROR
