@@ -1,0 +1,747 @@
+// psgpu_device.h — device code shared by the static kernels (psgpu_kernels.hip) and the
+// run-time specialised kernels (psgpu_jit.cpp, compiled with hiprtc).  Must compile
+// under hiprtc: no system headers.
+//
+// Reference semantics restated here (Parsip100/PS_SimdPoly/include/):
+//   computePrimitiveField           PS_Polygonizer.cpp:934-1179
+//   ComputeWyvillFieldValueSquare_  PS_Polygonizer.h:397-407
+//   FieldComputer::fieldValue       PS_Polygonizer.cpp:1184-1376 (op-box pruning :1228-1252)
+//   FieldComputer::fieldValueAndColor :1378-1551, normal :1598-1622
+//   CMPUProcessor::process_cells_simd :475-829
+// Every fp32 expression keeps the reference's operation order; builds use
+// -ffp-contract=off, IEEE division/sqrt (sqrtf, '/') and IEEE denormals.  max/min are the
+// SSE definitions (a>b?a:b, a<b?a:b; PS_SIMDVecN.h:388-389), masks are {0,1} multipliers.
+#pragma once
+#include "psgpu_model.h"
+
+namespace psgpu {
+
+// ---------------------------------------------------------------------------
+// The model is read through the constant address space so that every wave-uniform
+// access (walk program, op boxes, primitive parameters) is an s_load into SGPRs.
+typedef const __attribute__((address_space(4))) DevModel* ModelPtr;
+typedef const __attribute__((address_space(4))) DevPrim CPrim;
+typedef const __attribute__((address_space(4))) DevOp COp;
+typedef const __attribute__((address_space(4))) CubeTablesDev* TablePtr;
+__device__ __forceinline__ ModelPtr as_const(const DevModel* m) { return (ModelPtr)m; }
+__device__ __forceinline__ TablePtr as_const(const CubeTablesDev* t) { return (TablePtr)t; }
+
+__device__ __forceinline__ Instr load_instr(ModelPtr M, int pc) {
+    typedef const __attribute__((address_space(4))) uint32_t* CU32;
+    const CU32 w = (CU32)(&M->instr[pc]);
+    const uint32_t words[3] = {w[0], w[1], w[2]};
+    Instr I;
+    __builtin_memcpy(&I, words, 12);
+    return I;
+}
+
+__device__ __forceinline__ float max_ref(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float min_ref(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float m01(bool c) { return c ? 1.0f : 0.0f; }
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool v) { return __ballot(v); }
+
+// 1 if any lane of this lane's 4-lane group has v set (the reference's 4-wide SIMD
+// group: VecNMask(inside) == PS_SIMD_ALLZERO, PS_Polygonizer.cpp:1243).
+__device__ __forceinline__ bool quad_any(bool v) {
+    uint64_t b = ballot(v);
+    uint64_t t = b | (b >> 1);
+    t |= t >> 2;
+    t &= 0x1111111111111111ull;
+    t |= t << 1;
+    t |= t << 2;
+    return (t >> lane_id()) & 1ull;
+}
+
+template <int GROUP>
+__device__ __forceinline__ bool group_any(bool v) {
+    if (GROUP == 4) return quad_any(v);
+    return v;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Primitive fields.  dist2 per skeleton type, then Wyvill.
+template <int TYPE>
+__device__ __forceinline__ float prim_dist2(CPrim& P, float x, float y, float z) {
+    float d2 = 0.0f;
+    if (TYPE == PSGPU_T_POINT) {  // :975-983
+        float dx = P.pos[0] - x, dy = P.pos[1] - y, dz = P.pos[2] - z;
+        d2 = (dx * dx + dy * dy) + dz * dz;
+    } else if (TYPE == PSGPU_T_LINE) {  // :984-1011 (pos = start, dir = end), not clamped
+        float l0x = P.pos[0], l0y = P.pos[1], l0z = P.pos[2];
+        float ldx = P.dir[0] - l0x, ldy = P.dir[1] - l0y, ldz = P.dir[2] - l0z;
+        float ldd = (ldx * ldx + ldy * ldy) + ldz * ldz;
+        float dx = x - l0x, dy = y - l0y, dz = z - l0z;
+        float t = (dx * ldx + dy * ldy) + dz * ldz;
+        t = t / ldd;
+        dx = x - (l0x + t * ldx);
+        dy = y - (l0y + t * ldy);
+        dz = z - (l0z + t * ldz);
+        d2 = (dx * dx + dy * dy) + dz * dz;
+    } else if (TYPE == PSGPU_T_CYLINDER) {  // :1012-1039 (axis dir, r = resX, h = resY)
+        float px = x - P.pos[0], py = y - P.pos[1], pz = z - P.pos[2];
+        float yy = (px * P.dir[0] + py * P.dir[1]) + pz * P.dir[2];
+        float rr = ((px * px + py * py) + pz * pz) - yy * yy;
+        float xx = max_ref(0.0f, sqrtf(rr) - P.res[0]);
+        float mask = m01(yy > 0.0f);
+        yy = mask * max_ref(0.0f, yy - P.res[1]) + (1.0f - mask) * yy;
+        d2 = xx * xx + yy * yy;
+    } else if (TYPE == PSGPU_T_TRIANGLE) {  // :1040-1057 distance stub
+        d2 = 3.402823466e+38f;
+    } else if (TYPE == PSGPU_T_CUBE) {  // :1059-1097 (half side resX)
+        float side = P.res[0], mside = -1.0f * P.res[0];
+        float dif[3] = {x - P.pos[0], y - P.pos[1], z - P.pos[2]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float mm = m01(mside > dif[a]);
+            float mp = m01(dif[a] > side);
+            float dl = (dif[a] + side) * mm + (dif[a] - side) * mp;
+            d2 = (a == 0) ? dl * dl : d2 + dl * dl;
+        }
+    } else if (TYPE == PSGPU_T_DISC) {  // :1099-1132
+        float dX = x - P.pos[0], dY = y - P.pos[1], dZ = z - P.pos[2];
+        float nX = P.dir[0], nY = P.dir[1], nZ = P.dir[2], r = P.res[0];
+        float dot = (nX * dX + nY * dY) + nZ * dZ;
+        float rX = dX - nX * dot, rY = dY - nY * dot, rZ = dZ - nZ * dot;
+        dot = (rX * rX + rY * rY) + rZ * rZ;
+        float rs = 1.0f / sqrtf(dot);  // _mm_rsqrt_ps in the reference (vendor specific)
+        rX = rX * rs; rY = rY * rs; rZ = rZ * rs;
+        nX = r * rX - dX; nY = r * rY - dY; nZ = r * rZ - dZ;
+        float mask = m01(r * r >= dot);
+        d2 = mask * (((dX * dX + dY * dY) + dZ * dZ) - dot) + (1.0f - mask) * ((nX * nX + nY * nY) + nZ * nZ);
+    } else if (TYPE == PSGPU_T_RING) {  // :1134-1173
+        float dX = x - P.pos[0], dY = y - P.pos[1], dZ = z - P.pos[2];
+        float nX = P.dir[0], nY = P.dir[1], nZ = P.dir[2], r = P.res[0];
+        float dot = (nX * dX + nY * dY) + nZ * dZ;
+        float rX = dX - nX * dot, rY = dY - nY * dot, rZ = dZ - nZ * dot;
+        dot = (rX * rX + rY * rY) + rZ * rZ;
+        float mask = m01(dot == 0.0f);
+        dot = 1.0f / sqrtf(dot);
+        rX = rX * dot; rY = rY * dot; rZ = rZ * dot;
+        nX = r * rX - dX; nY = r * rY - dY; nZ = r * rZ - dZ;
+        d2 = mask * (((r * r + dX * dX) + dY * dY) + dZ * dZ) + (1.0f - mask) * ((nX * nX + nY * nY) + nZ * nZ);
+    }
+    // any other code: no case in the reference switch, dist2 stays 0 (field 1)
+    return d2;
+}
+
+__device__ __forceinline__ float wyvill(float d2) {
+    float t = 1.0f - d2;
+    float f = (t * t) * t;
+    return max_ref(0.0f, f);
+}
+
+template <int TYPE, bool MAT>
+__device__ __forceinline__ float prim_field_t(CPrim& P, float pX, float pY, float pZ) {
+    float x = pX, y = pY, z = pZ;
+    if (MAT) {  // :948-970, rows ((m0*x + m1*y) + m2*z) + m3
+        x = ((P.mat[0] * pX + P.mat[1] * pY) + P.mat[2] * pZ) + P.mat[3];
+        y = ((P.mat[4] * pX + P.mat[5] * pY) + P.mat[6] * pZ) + P.mat[7];
+        z = ((P.mat[8] * pX + P.mat[9] * pY) + P.mat[10] * pZ) + P.mat[11];
+    }
+    return wyvill(prim_dist2<TYPE>(P, x, y, z));
+}
+
+// run-time dispatch (interpreter)
+__device__ __forceinline__ float prim_field(CPrim& P, float pX, float pY, float pZ) {
+    float x = pX, y = pY, z = pZ;
+    if (P.hasMatrix) {
+        x = ((P.mat[0] * pX + P.mat[1] * pY) + P.mat[2] * pZ) + P.mat[3];
+        y = ((P.mat[4] * pX + P.mat[5] * pY) + P.mat[6] * pZ) + P.mat[7];
+        z = ((P.mat[8] * pX + P.mat[9] * pY) + P.mat[10] * pZ) + P.mat[11];
+    }
+    float d2;
+    switch (P.type) {
+    case PSGPU_T_POINT: d2 = prim_dist2<PSGPU_T_POINT>(P, x, y, z); break;
+    case PSGPU_T_LINE: d2 = prim_dist2<PSGPU_T_LINE>(P, x, y, z); break;
+    case PSGPU_T_CYLINDER: d2 = prim_dist2<PSGPU_T_CYLINDER>(P, x, y, z); break;
+    case PSGPU_T_TRIANGLE: d2 = prim_dist2<PSGPU_T_TRIANGLE>(P, x, y, z); break;
+    case PSGPU_T_CUBE: d2 = prim_dist2<PSGPU_T_CUBE>(P, x, y, z); break;
+    case PSGPU_T_DISC: d2 = prim_dist2<PSGPU_T_DISC>(P, x, y, z); break;
+    case PSGPU_T_RING: d2 = prim_dist2<PSGPU_T_RING>(P, x, y, z); break;
+    default: d2 = 0.0f; break;
+    }
+    return wyvill(d2);
+}
+
+// Binary op field (:1282-1338); `last` is the previous op's field (stale outField).
+__device__ __forceinline__ float op_field(uint32_t type, float lf, float rf, float resY, float last) {
+    switch (type) {
+    case PSGPU_T_BLEND: return lf + rf;
+    case PSGPU_T_RICCI: {  // fast_pow, PS_SIMDVecN.h:122-128 (rcp -> IEEE 1/x)
+        const float base = lf + rf;
+        float den = resY * base;
+        den = resY - den;
+        den = base + den;
+        return base * (1.0f / den);
+    }
+    case PSGPU_T_UNION: return max_ref(lf, rf);
+    case PSGPU_T_INTERSECT: return min_ref(lf, rf);
+    case PSGPU_T_DIF: return min_ref(lf, 1.0f - rf);
+    case PSGPU_T_SMOOTHDIF: return lf * (1.0f - rf);
+    case 22: case 23: case 24: case 25: return lf;  // warps: identity
+    default: return last;
+    }
+}
+
+// Op colour weights (:1472-1522); returns false when the op keeps a colour instead.
+__device__ __forceinline__ bool op_colour_weights(uint32_t type, float lf, float rf, float v, float* wl, float* wr) {
+    switch (type) {
+    case PSGPU_T_BLEND: case PSGPU_T_RICCI:
+        *wl = 2.0f * (0.5f + lf) - 1.0f;
+        *wr = 2.0f * (0.5f + rf) - 1.0f;
+        return true;
+    case PSGPU_T_UNION: case PSGPU_T_INTERSECT:
+        *wl = m01((v - lf) == 0.0f);
+        *wr = m01((v - rf) == 0.0f);
+        return true;
+    case PSGPU_T_DIF: case PSGPU_T_SMOOTHDIF:
+        *wl = m01(lf == v);
+        *wr = m01((1.0f - rf) == v);
+        return true;
+    default:
+        return false;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Exact culling (never changes a bit of output).  A primitive whose support cannot
+// reach any point of the wave has computed dist2 >= 1, i.e. field exactly +0, and
+// is not evaluated.  For the wave's AABB with centre c and half-diagonal h, every
+// point q has d(q) >= d(c) - h for the 1-Lipschitz distances of Point, infinite Line,
+// axis-aligned Cube and the capped Cylinder with |axis| = 1.  The host marks a prim
+// cullable only without a matrix and with finite, well-conditioned parameters;
+// Cylinder also needs the AABB clear of its infinite axis (where the reference's
+// sqrt of a rounded-negative value is NaN).  The margin d^2 >= 1.02 covers fp32
+// rounding of the reference formulas by orders of magnitude.  Triangle is a constant
+// +0 (dist2 = FLT_MAX) and is always culled.
+struct CullMask {
+    uint64_t lo, hi;
+};
+
+__device__ __forceinline__ float cull_dist(CPrim& P, float cx, float cy, float cz, float* axisDist) {
+    *axisDist = 1e30f;
+    switch (P.type) {
+    case PSGPU_T_POINT: {
+        float dx = cx - P.pos[0], dy = cy - P.pos[1], dz = cz - P.pos[2];
+        return __builtin_amdgcn_sqrtf(dx * dx + dy * dy + dz * dz);
+    }
+    case PSGPU_T_LINE: {
+        float ux = P.dir[0] - P.pos[0], uy = P.dir[1] - P.pos[1], uz = P.dir[2] - P.pos[2];
+        float dx = cx - P.pos[0], dy = cy - P.pos[1], dz = cz - P.pos[2];
+        float uu = ux * ux + uy * uy + uz * uz;
+        float t = (dx * ux + dy * uy + dz * uz) * __builtin_amdgcn_rcpf(uu);
+        float ex = dx - t * ux, ey = dy - t * uy, ez = dz - t * uz;
+        return __builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez);
+    }
+    case PSGPU_T_CYLINDER: {
+        float dx = cx - P.pos[0], dy = cy - P.pos[1], dz = cz - P.pos[2];
+        float yy = dx * P.dir[0] + dy * P.dir[1] + dz * P.dir[2];
+        float rr = dx * dx + dy * dy + dz * dz - yy * yy;
+        float rad = __builtin_amdgcn_sqrtf(rr > 0.0f ? rr : 0.0f);
+        *axisDist = rad;
+        float ex = rad - P.res[0];
+        ex = ex > 0.0f ? ex : 0.0f;
+        float ey = yy < 0.0f ? -yy : (yy > P.res[1] ? yy - P.res[1] : 0.0f);
+        return __builtin_amdgcn_sqrtf(ex * ex + ey * ey);
+    }
+    case PSGPU_T_CUBE: {
+        float s = P.res[0];
+        float d[3] = {cx - P.pos[0], cy - P.pos[1], cz - P.pos[2]};
+        float acc = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float e = fabsf(d[a]) - s;
+            e = e > 0.0f ? e : 0.0f;
+            acc += e * e;
+        }
+        return __builtin_amdgcn_sqrtf(acc);
+    }
+    default:
+        return 0.0f;
+    }
+}
+
+// Cull mask for an AABB given by wave-uniform bounds.  Lane l tests prims l, l+64.
+__device__ __forceinline__ CullMask cull_mask_box(ModelPtr M, float x0, float y0, float z0, float x1, float y1,
+                                                  float z1) {
+    CullMask cm{0ull, 0ull};
+    if (!(x1 - x0 < 1e30f && y1 - y0 < 1e30f && z1 - z0 < 1e30f)) return cm;
+    const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), cz = 0.5f * (z0 + z1);
+    const float hx = 0.5f * (x1 - x0), hy = 0.5f * (y1 - y0), hz = 0.5f * (z1 - z0);
+    const float h = __builtin_amdgcn_sqrtf(hx * hx + hy * hy + hz * hz) * 1.0001f + 1e-6f;
+    const int n = (int)M->ctPrims;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const int i = half * 64 + lane_id();
+        bool cull = false;
+        if (i < n) {
+            CPrim& P = M->prims[i];
+            if (P.cullable) {
+                float ad;
+                const float d = cull_dist(P, cx, cy, cz, &ad) - h;
+                cull = d > 0.0f && d * d >= 1.02f;
+                if (P.type == PSGPU_T_CYLINDER) cull = cull && (ad - h > 0.05f);
+            } else if (P.type == PSGPU_T_TRIANGLE) {
+                cull = true;
+            }
+        }
+        const uint64_t b = ballot(cull);
+        if (half == 0) cm.lo = b; else cm.hi = b;
+    }
+    return cm;
+}
+
+// Cull mask for the AABB of this wave's points (all 64 lanes must participate).
+__device__ __forceinline__ CullMask cull_mask_points(ModelPtr M, float px, float py, float pz, bool enable) {
+    if (!enable) return CullMask{0ull, 0ull};
+    // a NaN coordinate (fminf/fmaxf would hide it) disables culling for the wave
+    if (ballot(!(px == px) || !(py == py) || !(pz == pz)) != 0ull) return CullMask{0ull, 0ull};
+    return cull_mask_box(M, wave_min(px), wave_min(py), wave_min(pz), wave_max(px), wave_max(py), wave_max(pz));
+}
+
+__device__ __forceinline__ bool culled(const CullMask& cm, uint32_t i) {
+    return i < 64 ? ((cm.lo >> i) & 1ull) : ((cm.hi >> (i - 64)) & 1ull);
+}
+
+// ---------------------------------------------------------------------------
+// Interpreter evaluator: the flattened walk program of psgpu_model.h.
+//   GROUP 4: pruning decided per 4-lane group (S1/S2 quads, S4 edge samples)
+//   GROUP 1: per lane (S5: the reference evaluates 4 identical lanes)
+//   COLOR  : fieldValueAndColor's colour walk as well; no subtree is skipped and lanes
+//            inside a pruned subtree see field 0 for its prims and ops (the
+//            reference's never-written arrays, defined as zero).
+// `sl` is this lane's value stack in LDS (stride 64 floats; colour: 4 floats per slot).
+struct InterpEval {
+    ModelPtr M;
+    float* sl;
+    __device__ InterpEval(ModelPtr m, float* slots) : M(m), sl(slots) {}
+
+    template <int GROUP, bool COLOR>
+    __device__ __forceinline__ float eval(float px, float py, float pz, const CullMask& cm, float* colOut) const {
+        const int n = (int)M->nInstr;
+        const bool noOps = M->ctOps == 0;
+        int resume = 0;
+        float last = 0.0f, acc = 0.0f;
+        float lc0 = 0.0f, lc1 = 0.0f, lc2 = 0.0f;
+        constexpr int SW = COLOR ? 4 : 1;
+        for (int pc = 0; pc < n; ++pc) {
+            const Instr I = load_instr(M, pc);
+            const bool act = pc >= resume;
+            if (I.kind == kEnter) {
+                COp& O = M->ops[I.idx];
+                bool in = ((px >= O.lo[0]) & (O.hi[0] >= px)) | ((py >= O.lo[1]) & (O.hi[1] >= py)) |
+                          ((pz >= O.lo[2]) & (O.hi[2] >= pz));
+                bool anyIn = group_any<GROUP>(act && in);
+                bool prune = act && !anyIn;
+                if (prune) {
+                    resume = I.skipTo;
+                    sl[(I.out * SW) * 64] = 0.0f;
+                    last = 0.0f;
+                }
+                if (!COLOR) {
+                    if (ballot(pc + 1 >= resume) == 0ull) pc = I.skipTo - 1;
+                }
+            } else if (I.kind == kPrim) {
+                if (COLOR) {
+                    float f = 0.0f;
+                    if (act && !culled(cm, I.idx)) f = prim_field(M->prims[I.idx], px, py, pz);
+                    sl[(I.out * SW) * 64] = f;
+                } else if (act) {
+                    float f = 0.0f;
+                    if (!culled(cm, I.idx)) f = prim_field(M->prims[I.idx], px, py, pz);
+                    sl[I.out * 64] = f;
+                }
+            } else if (I.kind == kOp) {
+                if (COLOR || act) {
+                    const float lf = sl[(I.lslot * SW) * 64];
+                    const float rf = sl[(I.rslot * SW) * 64];
+                    float v = op_field(I.type, lf, rf, M->ops[I.idx].resY, last);
+                    if (COLOR && !act) v = 0.0f;
+                    sl[(I.out * SW) * 64] = v;
+                    if (act) last = v;
+                    if (COLOR) {
+                        float cl0, cl1, cl2, cr0, cr1, cr2;
+                        if (I.childKind & 2) {
+                            cl0 = sl[(I.lslot * 4 + 1) * 64]; cl1 = sl[(I.lslot * 4 + 2) * 64]; cl2 = sl[(I.lslot * 4 + 3) * 64];
+                        } else {
+                            CPrim& P = M->prims[I.L];
+                            cl0 = P.col[0]; cl1 = P.col[1]; cl2 = P.col[2];
+                        }
+                        if (I.childKind & 1) {
+                            cr0 = sl[(I.rslot * 4 + 1) * 64]; cr1 = sl[(I.rslot * 4 + 2) * 64]; cr2 = sl[(I.rslot * 4 + 3) * 64];
+                        } else {
+                            CPrim& P = M->prims[I.R];
+                            cr0 = P.col[0]; cr1 = P.col[1]; cr2 = P.col[2];
+                        }
+                        float wl, wr;
+                        if (op_colour_weights(I.type, lf, rf, v, &wl, &wr)) {
+                            lc0 = wl * cl0 + wr * cr0;
+                            lc1 = wl * cl1 + wr * cr1;
+                            lc2 = wl * cl2 + wr * cr2;
+                        } else if (I.type >= 22 && I.type <= 25) {
+                            lc0 = cl0; lc1 = cl1; lc2 = cl2;
+                        }
+                        sl[(I.out * 4 + 1) * 64] = lc0;
+                        sl[(I.out * 4 + 2) * 64] = lc1;
+                        sl[(I.out * 4 + 3) * 64] = lc2;
+                    }
+                }
+            } else {  // kSumPrim
+                float f = 0.0f;
+                if (!culled(cm, I.idx)) f = prim_field(M->prims[I.idx], px, py, pz);
+                acc = acc + f;
+            }
+        }
+        if (COLOR) {
+            if (noOps) {
+                CPrim& P = M->prims[0];
+                lc0 = P.col[0]; lc1 = P.col[1]; lc2 = P.col[2];
+            }
+            colOut[0] = lc0;
+            colOut[1] = lc1;
+            colOut[2] = lc2;
+        }
+        return noOps ? acc : last;
+    }
+};
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void mpu_origin(const Params& p, uint32_t m, float o[3]) {
+    const uint32_t k = m % p.dims[2];
+    const uint32_t j = (m / p.dims[2]) % p.dims[1];
+    const uint32_t i = m / (p.dims[2] * p.dims[1]);
+    o[0] = p.lo[0] + (float)i * p.side;
+    o[1] = p.lo[1] + (float)j * p.side;
+    o[2] = p.lo[2] + (float)k * p.side;
+}
+
+// S1: 8 corners per MPU, lanes 0-3 z = lo, lanes 4-7 z = lo + side; (x,y) lanes
+// (0,0),(1,0),(0,1),(1,1) (PS_Polygonizer.cpp:488-519).  256 threads = 32 MPUs.
+template <class EV>
+__device__ __forceinline__ void precheck_body(const Params& p, float* lds, uint32_t* waveMask) {
+    const int wave = threadIdx.x >> 6;
+    EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane_id());
+    const uint32_t local = (blockIdx.x * 256 + threadIdx.x) >> 3;
+    const bool valid = local < p.mpuCount;
+    const uint32_t m = p.mpuBegin + (valid ? local : 0);
+    float o[3];
+    mpu_origin(p, m, o);
+    const int c = threadIdx.x & 7;
+    const float X = (float)(c & 1), Y = (float)((c >> 1) & 1), Z = (float)(c >> 2);
+    const float px = X * p.side + o[0];
+    const float py = Y * p.side + o[1];
+    const float pz = Z * p.side + o[2];
+    const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+    const float f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
+    const uint64_t b = ballot(valid && f > 0.0f);
+    if (lane_id() == 0) {
+        uint32_t mk = 0;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) mk |= (((b >> (8 * g)) & 0xffull) != 0ull ? 1u : 0u) << g;
+        waveMask[wave] = mk;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        p.passMask[blockIdx.x] = waveMask[0] | (waveMask[1] << 8) | (waveMask[2] << 16) | (waveMask[3] << 24);
+}
+
+// Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
+// LDS per wave: fv[512] f32 | edgeVid[1536] u16 | cfg[344] u8 | vbase[344] u16 |
+//               tbase[344] u16 | value slots (interpreter only)
+constexpr int kLdsFv = 0;
+constexpr int kLdsEdge = 2048;
+constexpr int kLdsCfg = kLdsEdge + 1536 * 2;
+constexpr int kLdsVbase = kLdsCfg + 344;
+constexpr int kLdsTbase = kLdsVbase + 344 * 2;
+constexpr int kLdsSlots = ((kLdsTbase + 344 * 2) + 15) & ~15;
+
+// owner cell of an edge = the first cell in (i,j,k) order that lists it (every cell
+// containing a sign-changing edge lists it: SURVEY.md §8(a) a9)
+__device__ __forceinline__ bool owns_edge(int i, int j, int k, int sx, int sy, int sz, int ax) {
+    const int ox = ax == 0 ? sx : max(sx - 1, 0);
+    const int oy = ax == 1 ? sy : max(sy - 1, 0);
+    const int oz = ax == 2 ? sz : max(sz - 1, 0);
+    return ox == i && oy == j && oz == k;
+}
+
+template <class EV>
+__device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
+    const int wave = threadIdx.x >> 6;
+    const int lane = lane_id();
+    const uint32_t w = blockIdx.x * 4 + wave;
+    const uint32_t passCount = p.ctr->passCount;
+    if (w >= passCount) return;
+    unsigned char* base = smem + wave * (kLdsSlots + p.slotsPerLane * 64 * 4);
+    float* fv = reinterpret_cast<float*>(base + kLdsFv);
+    uint16_t* edgeVid = reinterpret_cast<uint16_t*>(base + kLdsEdge);
+    uint8_t* cellCfg = base + kLdsCfg;
+    uint16_t* cellV = reinterpret_cast<uint16_t*>(base + kLdsVbase);
+    uint16_t* cellT = reinterpret_cast<uint16_t*>(base + kLdsTbase);
+    ModelPtr M = as_const(p.model);
+    TablePtr tab = as_const(p.tables);
+    EV ev(M, reinterpret_cast<float*>(base + kLdsSlots) + lane);
+
+    const uint32_t m = __builtin_amdgcn_readfirstlane(p.passList[w]);
+    float o[3];
+    mpu_origin(p, m, o);
+    const float cs = p.cs;
+
+    // S2 (:550-610): fv[x][y][z], lane = y*8 + z; quads = 4 consecutive z
+    const int y = lane >> 3, z = lane & 7;
+    const float py = o[1] + (float)y * cs;
+    const float pz = o[2] + (float)z * cs;
+    CullMask cm{0ull, 0ull};
+    if (p.cull) {
+        const float e = 7.0f * cs;
+        cm = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
+    }
+    uint32_t inside = 0;
+    for (int x = 0; x < 8; ++x) {
+        const float px = o[0] + (float)x * cs;
+        const float f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
+        fv[x * 64 + lane] = f;
+        inside += __popcll(ballot(f >= 0.5f));
+    }
+    if (inside == 0 || inside == 512) {
+        if (lane == 0) p.counts[w] = make_uint2(0u, 0u);
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    // S3 pass 1: configs, owned (new) vertices and triangles per cell, wave scans
+    uint32_t carryV = 0, carryT = 0;
+    for (int q = 0; q < 6; ++q) {
+        const int c = q * 64 + lane;
+        const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+        uint32_t cfg = 0;
+        if (c < 343) {
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const int xx = i + ((cc >> 2) & 1), yy = j + ((cc >> 1) & 1), zz = k + (cc & 1);
+                cfg |= (fv[xx * 64 + yy * 8 + zz] >= 0.5f ? 1u : 0u) << cc;
+            }
+        }
+        uint32_t nv = 0, nt = 0;
+        if (cfg != 0 && cfg != 255) {
+            uint32_t seen = 0;
+            for (int e = 0; e < 16; ++e) {
+                const int ed = tab->tri[cfg][e];
+                if (ed < 0) break;
+                if ((seen >> ed) & 1u) continue;
+                seen |= 1u << ed;
+                const int c1 = tab->corner1[ed], ax = tab->axis[ed];
+                nv += owns_edge(i, j, k, i + ((c1 >> 2) & 1), j + ((c1 >> 1) & 1), k + (c1 & 1), ax) ? 1u : 0u;
+            }
+            nt = tab->ntri[cfg];
+        }
+        const uint32_t sv = wave_incl_scan(nv);
+        const uint32_t st = wave_incl_scan(nt);
+        if (c < 343) {
+            cellCfg[c] = (uint8_t)cfg;
+            cellV[c] = (uint16_t)(carryV + sv - nv);
+            cellT[c] = (uint16_t)(carryT + st - nt);
+        }
+        carryV += __shfl(sv, 63);
+        carryT += __shfl(st, 63);
+    }
+    const uint32_t V = carryV, T = carryT;
+    uint32_t qv = 0, qt = 0;
+    if (lane == 0) {
+        qv = atomicAdd(&p.ctr->vCount, V);
+        qt = atomicAdd(&p.ctr->tCount, T);
+        p.counts[w] = make_uint2(V, T);
+    }
+    qv = __shfl(qv, 0);
+    qt = __shfl(qt, 0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    // pass 2: vertex ids in the reference's discovery order, vertex records
+    for (int q = 0; q < 6; ++q) {
+        const int c = q * 64 + lane;
+        if (c >= 343) break;
+        const uint32_t cfg = cellCfg[c];
+        if (cfg == 0 || cfg == 255) continue;
+        const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+        uint32_t vid = cellV[c];
+        uint32_t seen = 0;
+        for (int e = 0; e < 16; ++e) {
+            const int ed = tab->tri[cfg][e];
+            if (ed < 0) break;
+            if ((seen >> ed) & 1u) continue;
+            seen |= 1u << ed;
+            const int c1 = tab->corner1[ed], ax = tab->axis[ed];
+            const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
+            if (owns_edge(i, j, k, sx, sy, sz, ax)) {
+                edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)vid;
+                const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
+                const uint32_t g = qv + vid;
+                if (g < p.vcap) p.vq[g] = VertexRec{w, vid | (key << 16)};
+                ++vid;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    // pass 3 (S6, :816-825): triangles in table order
+    for (int q = 0; q < 6; ++q) {
+        const int c = q * 64 + lane;
+        if (c >= 343) break;
+        const uint32_t cfg = cellCfg[c];
+        if (cfg == 0 || cfg == 255) continue;
+        const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+        const uint32_t tb = cellT[c];
+        const uint32_t nt = tab->ntri[cfg];
+        for (uint32_t t = 0; t < nt; ++t) {
+            uint32_t v[3];
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                const int ed = tab->tri[cfg][t * 3 + s];
+                const int c1 = tab->corner1[ed], ax = tab->axis[ed];
+                const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
+                v[s] = edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax];
+            }
+            const uint32_t g = qt + tb + t;
+            if (g < p.tcap) p.tq[g] = TriRec{w, tb + t, v[0] | (v[1] << 16), v[2]};
+        }
+    }
+}
+
+// Vertices: batches of 16 vertices per wavefront iteration, one quad per vertex.
+// Phase A (quad pruning): the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762)
+// Phase B (per-lane pruning): lane 0 = p with colour, lanes 1..3 = p + delta*e_a
+// (fieldValueAndColor + normal, :764-807).
+template <class EV>
+__device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
+    const int wave = threadIdx.x >> 6;
+    const int lane = lane_id();
+    ModelPtr M = as_const(p.model);
+    EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
+    const uint32_t nV = min(p.ctr->vCount, p.vcap);
+    const int j = lane & 3;
+    const float third = 1.0f / 3.0f;
+    const float r = (float)j * third;
+    const float delta = 0.001f;
+    const float inv = -1.0f / delta;
+    for (;;) {
+        uint32_t batch = 0;
+        if (lane == 0) batch = atomicAdd(&p.dequeue[0], 1u);
+        batch = __shfl(batch, 0);
+        const uint32_t v0 = batch * 16;
+        if (v0 >= nV) break;
+        uint32_t rec = v0 + (lane >> 2);
+        const bool valid = rec < nV;
+        if (!valid) rec = v0;
+        const VertexRec R = p.vq[rec];
+        const uint32_t m = p.passList[R.w];
+        float o[3];
+        mpu_origin(p, m, o);
+        const uint32_t key = R.vidKey >> 16;
+        const int sx = key & 7, sy = (key >> 3) & 7, sz = (key >> 6) & 7, ax = (key >> 9) & 3;
+        const float cs = p.cs;
+        // e1 = lo + cs*s, e2 = e1 with e2[axis] += cs (:722-724)
+        float e1[3] = {o[0] + cs * (float)sx, o[1] + cs * (float)sy, o[2] + cs * (float)sz};
+        float e2[3] = {e1[0], e1[1], e1[2]};
+        e2[ax] = e1[ax] + cs;
+        const float dX = e2[0] - e1[0], dY = e2[1] - e1[1], dZ = e2[2] - e1[2];
+        const float qx = e1[0] + dX * r, qy = e1[1] + dY * r, qz = e1[2] + dZ * r;
+        const CullMask cm = cull_mask_points(M, qx, qy, qz, p.cull != 0);
+        const float f = ev.template eval<4, false>(qx, qy, qz, cm, nullptr);
+        const int qb = lane & ~3;
+        float fs[4], xs[4], ys[4], zs[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            fs[s] = __shfl(f, qb + s);
+            const float rs = (float)s * third;
+            xs[s] = e1[0] + dX * rs;
+            ys[s] = e1[1] + dY * rs;
+            zs[s] = e1[2] + dZ * rs;
+        }
+        // first sample whose inside state differs from sample 0, else 3 (:744-755)
+        const bool st0 = fs[0] >= 0.5f;
+        const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
+        const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
+        const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
+        const float ax0 = iv == 1 ? xs[0] : (iv == 2 ? xs[1] : xs[2]);
+        const float ay0 = iv == 1 ? ys[0] : (iv == 2 ? ys[1] : ys[2]);
+        const float az0 = iv == 1 ? zs[0] : (iv == 2 ? zs[1] : zs[2]);
+        const float bx0 = iv == 1 ? xs[1] : (iv == 2 ? xs[2] : xs[3]);
+        const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
+        const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
+        const float scale = (0.5f - fa) / (fb - fa);
+        const float P0 = ax0 + scale * (bx0 - ax0);
+        const float P1 = ay0 + scale * (by0 - ay0);
+        const float P2 = az0 + scale * (bz0 - az0);
+        const float qx2 = j == 1 ? P0 + delta : P0;
+        const float qy2 = j == 2 ? P1 + delta : P1;
+        const float qz2 = j == 3 ? P2 + delta : P2;
+        const CullMask cm2 = cull_mask_points(M, qx2, qy2, qz2, p.cull != 0);
+        float colr[3];
+        const float g = ev.template eval<1, true>(qx2, qy2, qz2, cm2, colr);
+        const float vtx = __shfl(g, qb);
+        const float gx = __shfl(g, qb + 1), gy = __shfl(g, qb + 2), gz = __shfl(g, qb + 3);
+        float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
+        const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);  // SimdNormalize
+        nx = nx * im;
+        ny = ny * im;
+        nz = nz * im;
+        if (valid && j == 0) {
+            const uint32_t gi = p.voff[R.w] + (R.vidKey & 0xffffu);
+            p.pos[gi * 3 + 0] = P0; p.pos[gi * 3 + 1] = P1; p.pos[gi * 3 + 2] = P2;
+            p.nrm[gi * 3 + 0] = nx; p.nrm[gi * 3 + 1] = ny; p.nrm[gi * 3 + 2] = nz;
+            p.col[gi * 3 + 0] = colr[0]; p.col[gi * 3 + 1] = colr[1]; p.col[gi * 3 + 2] = colr[2];
+        }
+    }
+}
+
+// Field probe for tests: mode 0 quads of consecutive points, 1 per point, 2 + colour.
+template <class EV>
+__device__ __forceinline__ void probe_body(const Params& p, float* lds, const float* xyz, float* out, float* colOut,
+                                           uint32_t n, int mode) {
+    const int wave = threadIdx.x >> 6;
+    ModelPtr M = as_const(p.model);
+    EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane_id());
+    uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const bool valid = i < n;
+    if (!valid) i = (n ? n - 1 : 0);
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    const CullMask cm = cull_mask_points(M, x, y, z, p.cull != 0);
+    float c[3] = {0.0f, 0.0f, 0.0f};
+    float f;
+    if (mode == 0) f = ev.template eval<4, false>(x, y, z, cm, nullptr);
+    else if (mode == 1) f = ev.template eval<1, false>(x, y, z, cm, nullptr);
+    else f = ev.template eval<1, true>(x, y, z, cm, c);
+    if (valid) {
+        out[i] = f;
+        if (colOut) {
+            colOut[3 * i] = c[0];
+            colOut[3 * i + 1] = c[1];
+            colOut[3 * i + 2] = c[2];
+        }
+    }
+}
+
+}  // namespace psgpu

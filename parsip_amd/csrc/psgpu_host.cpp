@@ -11,10 +11,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/parsip_gpu.h"
+#include "psgpu_jit.h"
 #include "psgpu_launch.h"
 #include "psgpu_model.h"
 
@@ -267,6 +270,10 @@ struct psgpu_ctx {
     PsSoaBlobPrims primsHost;  // bbox + counts of the current model
     DevModel model{};
     DevModel* dModel = nullptr;
+    CubeTablesDev* dTables = nullptr;
+    int useJit = 1;
+    std::shared_ptr<JitKernels> jit;   // specialised kernels of the current model
+    std::string jitError;
     bool haveModel = false;
     int cull = 1;
     int timing = 0;
@@ -335,6 +342,7 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
 Params make_params(psgpu_ctx* c) {
     Params p{};
     p.model = c->dModel;
+    p.tables = c->dTables;
     p.cs = c->cs;
     p.side = c->cs * (float)PSGPU_CELLS_PER_MPU;
     p.lo[0] = c->primsHost.bboxLo.x;
@@ -359,8 +367,13 @@ Params make_params(psgpu_ctx* c) {
     p.tris = c->tris;
     p.ctr = c->ctr;
     p.dequeue = c->dequeue;
-    p.slotsPerLane = c->model.nSlots;
+    p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     return p;
+}
+
+hipError_t launch_jit(hipFunction_t f, uint32_t blocks, uint32_t threads, size_t lds, hipStream_t s, Params& p) {
+    void* args[] = {&p};
+    return hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, (unsigned)lds, s, args, nullptr);
 }
 
 int enqueue(psgpu_ctx* c, hipStream_t s) {
@@ -369,17 +382,21 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     PSGPU_CHECK(hipMemsetAsync(c->dequeue, 0, 4 * sizeof(uint32_t), s));
     const bool t = c->timing != 0;
     const uint32_t persist = (uint32_t)c->numCUs * 4;
+    JitKernels* J = c->jit.get();
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     if (c->mpuCount > 0) {
-        PSGPU_CHECK(launch_precheck(p, s));
+        if (J) PSGPU_CHECK(launch_jit(J->precheck, (p.mpuCount + 31) / 32, 256, 0, s, p));
+        else PSGPU_CHECK(launch_precheck(p, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
         PSGPU_CHECK(launch_compact(p, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
-        PSGPU_CHECK(launch_mpu(p, s));
+        if (J) PSGPU_CHECK(launch_jit(J->mpu, (p.mpuCount + 3) / 4, 256, mpu_lds_bytes(0), s, p));
+        else PSGPU_CHECK(launch_mpu(p, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
         PSGPU_CHECK(launch_scan(p, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
-        PSGPU_CHECK(launch_vertex(p, s, persist));
+        if (J) PSGPU_CHECK(launch_jit(J->vertex, persist, 256, 0, s, p));
+        else PSGPU_CHECK(launch_vertex(p, s, persist));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
         PSGPU_CHECK(launch_tris(p, s, persist));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[6], s));
@@ -559,8 +576,14 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (hipGetDeviceProperties(&prop, deviceOrdinal) == hipSuccess && prop.multiProcessorCount > 0)
         c->numCUs = prop.multiProcessorCount;
     const CubeTables& T = cube_tables();
+    CubeTablesDev tabHost{};
+    memcpy(tabHost.tri, T.tri, sizeof(tabHost.tri));
+    memcpy(tabHost.ntri, T.ntri, sizeof(tabHost.ntri));
+    memcpy(tabHost.corner1, T.corner1, sizeof(tabHost.corner1));
+    memcpy(tabHost.axis, T.axis, sizeof(tabHost.axis));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        upload_tables(T.tri, T.ntri, T.corner1, T.axis) != hipSuccess ||
+        hipMalloc(&c->dTables, sizeof(CubeTablesDev)) != hipSuccess ||
+        hipMemcpy(c->dTables, &tabHost, sizeof(CubeTablesDev), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&c->dModel, sizeof(DevModel)) != hipSuccess ||
         hipMalloc(&c->ctr, sizeof(DevCounters)) != hipSuccess ||
         hipMalloc(&c->dequeue, 4 * sizeof(uint32_t)) != hipSuccess ||
@@ -574,6 +597,8 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     for (int i = 0; i <= kNumKernels; ++i) (void)hipEventCreate(&c->ev[i]);
     const char* cullEnv = getenv("PSGPU_CULL");
     if (cullEnv) c->cull = atoi(cullEnv) != 0;
+    const char* jitEnv = getenv("PSGPU_JIT");
+    if (jitEnv) c->useJit = atoi(jitEnv) != 0;
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -582,7 +607,8 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->dModel, c->passMask, c->passList, c->counts, c->voff, c->toff, c->vq, c->tq,
+    c->jit.reset();
+    void* bufs[] = {c->dModel, c->dTables, c->passMask, c->passList, c->counts, c->voff, c->toff, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->dequeue};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -598,6 +624,14 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (!c) return PSGPU_RET_PARAM_ERROR;
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
+    else if (option == PSGPU_OPT_JIT) {
+        c->useJit = value != 0;
+        if (!c->useJit) c->jit.reset();
+        else if (c->haveModel) {
+            c->jit = jit_get(c->model, c->device, &c->jitError);
+            if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
+        }
+    }
     else return PSGPU_RET_PARAM_ERROR;
     return PSGPU_RET_SUCCESS;
 }
@@ -617,6 +651,11 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
     PSGPU_CHECK(hipStreamSynchronize(c->stream));
     c->haveModel = true;
+    c->jit.reset();
+    if (c->useJit) {
+        c->jit = jit_get(c->model, c->device, &c->jitError);
+        if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
+    }
     return PSGPU_RET_SUCCESS;
 }
 
@@ -821,7 +860,13 @@ int psgpu_field_values(psgpu_ctx* c, const float* xyz, uint32_t n, int mode, flo
     PSGPU_CHECK(hipMalloc(&dcol, (size_t)n * 12));
     PSGPU_CHECK(hipMemcpy(dx, xyz, (size_t)n * 12, hipMemcpyHostToDevice));
     Params p = make_params(c);
-    hipError_t e = launch_probe(p, c->stream, dx, dout, dcol, n, mode);
+    hipError_t e;
+    if (c->jit) {
+        void* args[] = {&p, &dx, &dout, &dcol, &n, &mode};
+        e = hipModuleLaunchKernel(c->jit->probe, (n + 255) / 256, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr);
+    } else {
+        e = launch_probe(p, c->stream, dx, dout, dcol, n, mode);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
     if (e == hipSuccess && colOut) e = hipMemcpy(colOut, dcol, (size_t)n * 12, hipMemcpyDeviceToHost);
@@ -829,6 +874,39 @@ int psgpu_field_values(psgpu_ctx* c, const float* xyz, uint32_t n, int mode, flo
     (void)hipFree(dout);
     (void)hipFree(dcol);
     return hip_fail(e, "psgpu_field_values");
+}
+
+// Host-only: build the device image of a model and compile its specialised kernels
+// (no GPU needed).  Returns the code-object size, or a negative error code.
+long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats, const PsSoaBlobOps* ops,
+                       char* log, size_t cap) {
+    if (!prims || !mats || !ops) return PSGPU_RET_PARAM_ERROR;
+    std::unique_ptr<DevModel> m(new DevModel);
+    int rc = build_device_model(*prims, *mats, *ops, *m);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    std::string err;
+    long n = jit_compile_only(*m, &err);
+    if (log && cap) {
+        const size_t k = std::min(cap - 1, err.size());
+        memcpy(log, err.data(), k);
+        log[k] = 0;
+    }
+    return n < 0 ? PSGPU_RET_DEVICE_ERROR : n;
+}
+
+// Whether the current model runs on run-time specialised kernels (1) or the interpreter (0).
+int psgpu_jit_active(psgpu_ctx* c) { return c && c->jit ? 1 : 0; }
+
+// Generated specialised source for the current model (NUL-terminated, truncated to cap).
+int psgpu_jit_source(psgpu_ctx* c, char* buf, size_t cap) {
+    if (!c || !c->haveModel) return PSGPU_RET_PARAM_ERROR;
+    const std::string s = jit_source(c->model);
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, s.size());
+        memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int)s.size();
 }
 
 }  // extern "C"

@@ -8,8 +8,6 @@
 
 namespace psgpu {
 
-hipError_t upload_tables(const int8_t tri[256][16], const uint8_t ntri[256], const uint8_t corner1[12],
-                         const uint8_t axis[12]);
 size_t mpu_lds_bytes(uint32_t slots);
 size_t walk_lds_bytes(uint32_t slots);
 size_t precheck_lds_bytes(uint32_t slots);

@@ -17,10 +17,44 @@
 // first, :1344-1352), which also fixes the "stale outField" semantics of op types
 // that have no case in the reference switch.
 #pragma once
+#ifdef __HIPCC_RTC__
+// hiprtc (run-time specialised kernels, psgpu_jit.cpp): no system headers
+typedef unsigned char uint8_t;
+typedef signed char int8_t;
+typedef unsigned short uint16_t;
+typedef unsigned int uint32_t;
+typedef int int32_t;
+typedef unsigned long long uint64_t;
+#else
 #include <stdint.h>
 #include <hip/hip_runtime.h>
+#endif
 
 namespace psgpu {
+
+// Node type codes of the hot path (PS_Polygonizer.h:84-91; same as PsNodeType).
+#define PSGPU_T_CYLINDER 0
+#define PSGPU_T_DISC 1
+#define PSGPU_T_LINE 2
+#define PSGPU_T_POINT 3
+#define PSGPU_T_RING 4
+#define PSGPU_T_CUBE 6
+#define PSGPU_T_TRIANGLE 7
+#define PSGPU_T_UNION 14
+#define PSGPU_T_INTERSECT 15
+#define PSGPU_T_DIF 16
+#define PSGPU_T_SMOOTHDIF 17
+#define PSGPU_T_BLEND 18
+#define PSGPU_T_RICCI 19
+
+// Marching-cubes tables in device memory (generated on the host, psgpu_host.cpp).
+struct CubeTablesDev {
+    int8_t tri[256][16];
+    uint8_t ntri[256];
+    uint8_t corner1[12];
+    uint8_t axis[12];
+    uint8_t pad[8];
+};
 
 enum InstrKind : uint8_t { kEnter = 0, kPrim = 1, kOp = 2, kSumPrim = 3 };
 
@@ -99,6 +133,7 @@ struct DevCounters {
 // Kernel arguments of one polygonization (one struct, passed by value).
 struct Params {
     const DevModel* __restrict__ model;
+    const CubeTablesDev* __restrict__ tables;
     float cs;           // cellsize
     float side;         // cellsize * 7.0f (MPU side)
     float lo[3];        // scene bboxLo

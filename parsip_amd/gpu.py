@@ -43,8 +43,12 @@ EXPORTED_SYMBOLS = [
     "psgpu_tritable", "psgpu_version", "psgpu_create", "psgpu_destroy", "psgpu_device_count",
     "psgpu_set_model", "psgpu_polygonize", "psgpu_finish", "psgpu_mesh_device", "psgpu_download_mesh",
     "psgpu_download_stats", "psgpu_export_polympus", "psgpu_polygonize_mpus", "psgpu_last_kernel_times",
-    "psgpu_field_values", "psgpu_set_option",
+    "psgpu_field_values", "psgpu_set_option", "psgpu_jit_active", "psgpu_jit_source", "psgpu_jit_compile",
 ]
+
+OPT_KERNEL_TIMING = 1
+OPT_CULLING = 2
+OPT_JIT = 3
 
 
 def load(build_if_missing: bool = True):
@@ -78,6 +82,9 @@ def load(build_if_missing: bool = True):
         "psgpu_last_kernel_times": ([vp, vp, i32, vp], i32),
         "psgpu_field_values": ([vp, vp, u32, i32, vp, vp], i32),
         "psgpu_set_option": ([vp, i32, ctypes.c_int64], i32),
+        "psgpu_jit_active": ([vp], i32),
+        "psgpu_jit_source": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
+        "psgpu_jit_compile": ([vp, vp, vp, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -118,6 +125,15 @@ def tritable() -> np.ndarray:
     t = np.zeros((256, 16), np.int32)
     load().psgpu_tritable(t.ctypes.data)
     return t
+
+
+def jit_compile(model: soa.Model) -> int:
+    """Host-only: compile the model's specialised kernels (hiprtc); returns code size."""
+    log = ctypes.create_string_buffer(1 << 16)
+    n = load().psgpu_jit_compile(*model.ptrs(), log, len(log))
+    if n < 0:
+        raise PsgpuError(n, "psgpu_jit_compile: " + log.value.decode(errors="replace"))
+    return n
 
 
 def device_count() -> int:
@@ -165,6 +181,16 @@ class Polygonizer:
 
     def set_option(self, option: int, value: int) -> None:
         _check(self._L.psgpu_set_option(self._ctx, option, value), "psgpu_set_option")
+
+    @property
+    def jit_active(self) -> bool:
+        return bool(self._L.psgpu_jit_active(self._ctx))
+
+    def jit_source(self) -> str:
+        n = self._L.psgpu_jit_source(self._ctx, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        self._L.psgpu_jit_source(self._ctx, buf, n + 1)
+        return buf.value.decode()
 
     def set_model(self, model: soa.Model) -> None:
         p, m, o = model.ptrs()

@@ -16,9 +16,11 @@ from parsip_amd.soa import NodeType
 pytestmark = pytest.mark.gpu
 
 
-def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1):
-    poly.set_option(2, cull)
+def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1, jit=1):
+    poly.set_option(gpu.OPT_CULLING, cull)
+    poly.set_option(gpu.OPT_JIT, jit)
     poly.set_model(model)
+    assert poly.jit_active == bool(jit)
     poly.run(cs, begin, end)
     gm = poly.download()
     gs = poly.stats()
@@ -28,9 +30,10 @@ def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1):
 
 @pytest.mark.parametrize("name", ["C1", "C2"])
 @pytest.mark.parametrize("cull", [0, 1])
-def test_configs_bit_exact(gpu_poly, oracle, name, cull):
+@pytest.mark.parametrize("jit", [0, 1])
+def test_configs_bit_exact(gpu_poly, oracle, name, cull, jit):
     model, cs, _ = synth.make_config(name)
-    gm, gs, om = run_both(gpu_poly, oracle, model, cs, cull=cull)
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs, cull=cull, jit=jit)
     assert len(gm.pos) > 0
     assert_mesh_matches(gm, gs, om)
 
@@ -48,6 +51,13 @@ def test_c3_full_size(gpu_poly, oracle):
     """Headline workload (256^3, 32 prims, pruning live) against the oracle, in full."""
     model, cs, _ = synth.make_config("C3")
     gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert_mesh_matches(gm, gs, om)
+
+
+@pytest.mark.parametrize("jit", [0, 1])
+def test_c3_interpreter_and_jit(gpu_poly, oracle, jit):
+    model, cs, _ = synth.make_config("C3")
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs, jit=jit)
     assert_mesh_matches(gm, gs, om)
 
 
