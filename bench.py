@@ -108,17 +108,22 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
+    ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
+                    help="0 interpreter, 1 kernels specialised per tree structure, 2 + parameters baked in")
     args = ap.parse_args()
 
     grp = Group()
     poly = gpu.Polygonizer(grp.local)  # HIP device initialised before torch is imported
     grp.init()
     if args.no_cull:
-        poly.set_option(2, 0)
+        poly.set_option(gpu.OPT_CULLING, 0)
+    poly.set_option(gpu.OPT_JIT, args.jit)
 
     frame = grp.rank if args.scaling == "weak" else 0
     model, cs, N = synth.make_config(args.config, frame=frame)
-    poly.set_model(model)
+    t_model = time.perf_counter()
+    poly.set_model(model)  # uploads the SoA and builds/compiles the tree kernels
+    t_model = time.perf_counter() - t_model
     n_mpus = gpu.count_mpus(cs, *model.bbox)
     if args.scaling == "strong" and grp.world > 1:
         per = (n_mpus + grp.world - 1) // grp.world
@@ -175,7 +180,9 @@ def main():
                                f"{n_mpus} MPUs" + (f", frame=rank" if args.scaling == "weak" and grp.world > 1 else ""),
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,
                    "parallelism": f"{args.scaling}-{grp.world}gpu",
-                   "mpu_range": [begin, end], "culling": not args.no_cull},
+                   "mpu_range": [begin, end], "culling": not args.no_cull,
+                   "kernels": ["interpreter", "jit-structure", "jit-baked"][args.jit] if poly.jit_active or args.jit == 0
+                   else "interpreter (jit unavailable)", "set_model_s": round(t_model, 3)},
         "roofline": {"bound": "mfma", "pipe": "fp32 VALU (peak = FP32 vector = FP32 MFMA rate)",
                      "kernel": dom, "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / VALU_PEAK_TFLOPS, 4), "traffic": None,

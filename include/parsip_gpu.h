@@ -216,11 +216,13 @@ int  psgpu_field_values(psgpu_ctx* ctx, const float* xyz, uint32_t n, int mode, 
 int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_KERNEL_TIMING 1   /* 1: record hipEvents around every kernel */
 #define PSGPU_OPT_CULLING       2   /* 1: exact per-wave primitive culling (default) */
-#define PSGPU_OPT_JIT           3   /* 1: run-time specialised tree kernels (default) */
-/* Host-only (no GPU): compile the model's specialised kernels with hiprtc; returns the
- * code-object size or a negative error (log receives the compiler output). */
+#define PSGPU_OPT_JIT           3   /* 0 interpreter, 1 specialised per structure (default),
+                                       2 specialised with parameters baked in */
+/* Host-only (no GPU): compile the model's specialised kernels with hiprtc (mode 1:
+ * structure only, 2: parameters baked in); returns the code-object size or a negative
+ * error (log receives the compiler output). */
 long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* matrices,
-                       const PsSoaBlobOps* ops, char* log, size_t cap);
+                       const PsSoaBlobOps* ops, int mode, char* log, size_t cap);
 /* 1 if the current model runs on run-time specialised kernels, 0 on the interpreter. */
 int  psgpu_jit_active(psgpu_ctx* ctx);
 /* Generated specialised HIP source of the current model; returns its length. */

@@ -43,14 +43,12 @@ __device__ __forceinline__ uint64_t ballot(bool v) { return __ballot(v); }
 
 // 1 if any lane of this lane's 4-lane group has v set (the reference's 4-wide SIMD
 // group: VecNMask(inside) == PS_SIMD_ALLZERO, PS_Polygonizer.cpp:1243).
+// DPP quad_perm swaps within each 4-lane group: [1,0,3,2] then [2,3,0,1].
 __device__ __forceinline__ bool quad_any(bool v) {
-    uint64_t b = ballot(v);
-    uint64_t t = b | (b >> 1);
-    t |= t >> 2;
-    t &= 0x1111111111111111ull;
-    t |= t << 1;
-    t |= t << 2;
-    return (t >> lane_id()) & 1ull;
+    int x = v ? 1 : 0;
+    x |= __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
+    return x != 0;
 }
 
 template <int GROUP>
@@ -81,8 +79,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 // ---------------------------------------------------------------------------
 // Primitive fields.  dist2 per skeleton type, then Wyvill.
-template <int TYPE>
-__device__ __forceinline__ float prim_dist2(CPrim& P, float x, float y, float z) {
+// PR: a DevPrim in the constant address space (parameters loaded at run time) or a
+// constexpr BakedPrim (parameters compiled into the code, psgpu_jit.cpp mode 2).
+struct BakedPrim {
+    float pos[3], dir[3], res[3], col[3], mat[12];
+};
+struct BakedOp {
+    float lo[3], hi[3], resY;
+};
+
+template <int TYPE, class PR>
+__device__ __forceinline__ float prim_dist2(PR& P, float x, float y, float z) {
     float d2 = 0.0f;
     if (TYPE == PSGPU_T_POINT) {  // :975-983
         float dx = P.pos[0] - x, dy = P.pos[1] - y, dz = P.pos[2] - z;
@@ -151,15 +158,15 @@ __device__ __forceinline__ float wyvill(float d2) {
     return max_ref(0.0f, f);
 }
 
-template <int TYPE, bool MAT>
-__device__ __forceinline__ float prim_field_t(CPrim& P, float pX, float pY, float pZ) {
+template <int TYPE, bool MAT, class PR>
+__device__ __forceinline__ float prim_field_t(PR& P, float pX, float pY, float pZ) {
     float x = pX, y = pY, z = pZ;
     if (MAT) {  // :948-970, rows ((m0*x + m1*y) + m2*z) + m3
         x = ((P.mat[0] * pX + P.mat[1] * pY) + P.mat[2] * pZ) + P.mat[3];
         y = ((P.mat[4] * pX + P.mat[5] * pY) + P.mat[6] * pZ) + P.mat[7];
         z = ((P.mat[8] * pX + P.mat[9] * pY) + P.mat[10] * pZ) + P.mat[11];
     }
-    return wyvill(prim_dist2<TYPE>(P, x, y, z));
+    return wyvill(prim_dist2<TYPE, PR>(P, x, y, z));
 }
 
 // run-time dispatch (interpreter)
@@ -172,13 +179,13 @@ __device__ __forceinline__ float prim_field(CPrim& P, float pX, float pY, float 
     }
     float d2;
     switch (P.type) {
-    case PSGPU_T_POINT: d2 = prim_dist2<PSGPU_T_POINT>(P, x, y, z); break;
-    case PSGPU_T_LINE: d2 = prim_dist2<PSGPU_T_LINE>(P, x, y, z); break;
-    case PSGPU_T_CYLINDER: d2 = prim_dist2<PSGPU_T_CYLINDER>(P, x, y, z); break;
-    case PSGPU_T_TRIANGLE: d2 = prim_dist2<PSGPU_T_TRIANGLE>(P, x, y, z); break;
-    case PSGPU_T_CUBE: d2 = prim_dist2<PSGPU_T_CUBE>(P, x, y, z); break;
-    case PSGPU_T_DISC: d2 = prim_dist2<PSGPU_T_DISC>(P, x, y, z); break;
-    case PSGPU_T_RING: d2 = prim_dist2<PSGPU_T_RING>(P, x, y, z); break;
+    case PSGPU_T_POINT: d2 = prim_dist2<PSGPU_T_POINT, CPrim>(P, x, y, z); break;
+    case PSGPU_T_LINE: d2 = prim_dist2<PSGPU_T_LINE, CPrim>(P, x, y, z); break;
+    case PSGPU_T_CYLINDER: d2 = prim_dist2<PSGPU_T_CYLINDER, CPrim>(P, x, y, z); break;
+    case PSGPU_T_TRIANGLE: d2 = prim_dist2<PSGPU_T_TRIANGLE, CPrim>(P, x, y, z); break;
+    case PSGPU_T_CUBE: d2 = prim_dist2<PSGPU_T_CUBE, CPrim>(P, x, y, z); break;
+    case PSGPU_T_DISC: d2 = prim_dist2<PSGPU_T_DISC, CPrim>(P, x, y, z); break;
+    case PSGPU_T_RING: d2 = prim_dist2<PSGPU_T_RING, CPrim>(P, x, y, z); break;
     default: d2 = 0.0f; break;
     }
     return wyvill(d2);
@@ -312,12 +319,15 @@ __device__ __forceinline__ CullMask cull_mask_box(ModelPtr M, float x0, float y0
     return cm;
 }
 
-// Cull mask for the AABB of this wave's points (all 64 lanes must participate).
-__device__ __forceinline__ CullMask cull_mask_points(ModelPtr M, float px, float py, float pz, bool enable) {
+// Cull mask for the AABB of this wave's points (all 64 lanes must participate),
+// optionally grown by `ext` on the high side of every axis.
+__device__ __forceinline__ CullMask cull_mask_points(ModelPtr M, float px, float py, float pz, bool enable,
+                                                     float ext = 0.0f) {
     if (!enable) return CullMask{0ull, 0ull};
     // a NaN coordinate (fminf/fmaxf would hide it) disables culling for the wave
     if (ballot(!(px == px) || !(py == py) || !(pz == pz)) != 0ull) return CullMask{0ull, 0ull};
-    return cull_mask_box(M, wave_min(px), wave_min(py), wave_min(pz), wave_max(px), wave_max(py), wave_max(pz));
+    return cull_mask_box(M, wave_min(px), wave_min(py), wave_min(pz), wave_max(px) + ext, wave_max(py) + ext,
+                         wave_max(pz) + ext);
 }
 
 __device__ __forceinline__ bool culled(const CullMask& cm, uint32_t i) {
@@ -598,7 +608,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
                 edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)vid;
                 const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
                 const uint32_t g = qv + vid;
-                if (g < p.vcap) p.vq[g] = VertexRec{w, vid | (key << 16)};
+                if (g < p.vcap) p.vq[g] = VertexRec{w, m, vid | (key << 16), 0u};
                 ++vid;
             }
         }
@@ -646,17 +656,16 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const float r = (float)j * third;
     const float delta = 0.001f;
     const float inv = -1.0f / delta;
-    for (;;) {
-        uint32_t batch = 0;
-        if (lane == 0) batch = atomicAdd(&p.dequeue[0], 1u);
-        batch = __shfl(batch, 0);
+    const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave;; batch += nWaves) {
         const uint32_t v0 = batch * 16;
         if (v0 >= nV) break;
         uint32_t rec = v0 + (lane >> 2);
         const bool valid = rec < nV;
         if (!valid) rec = v0;
         const VertexRec R = p.vq[rec];
-        const uint32_t m = p.passList[R.w];
+        const uint32_t outBase = p.voff[R.w];  // consumed at the end: latency overlaps the walk
+        const uint32_t m = R.m;
         float o[3];
         mpu_origin(p, m, o);
         const uint32_t key = R.vidKey >> 16;
@@ -668,7 +677,8 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         e2[ax] = e1[ax] + cs;
         const float dX = e2[0] - e1[0], dY = e2[1] - e1[1], dZ = e2[2] - e1[2];
         const float qx = e1[0] + dX * r, qy = e1[1] + dY * r, qz = e1[2] + dZ * r;
-        const CullMask cm = cull_mask_points(M, qx, qy, qz, p.cull != 0);
+        // one cull box for both phases: the edge samples' AABB grown by delta covers p + delta*e_a
+        const CullMask cm = cull_mask_points(M, qx, qy, qz, p.cull != 0, delta);
         const float f = ev.template eval<4, false>(qx, qy, qz, cm, nullptr);
         const int qb = lane & ~3;
         float fs[4], xs[4], ys[4], zs[4];
@@ -698,9 +708,8 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         const float qx2 = j == 1 ? P0 + delta : P0;
         const float qy2 = j == 2 ? P1 + delta : P1;
         const float qz2 = j == 3 ? P2 + delta : P2;
-        const CullMask cm2 = cull_mask_points(M, qx2, qy2, qz2, p.cull != 0);
         float colr[3];
-        const float g = ev.template eval<1, true>(qx2, qy2, qz2, cm2, colr);
+        const float g = ev.template eval<1, true>(qx2, qy2, qz2, cm, colr);
         const float vtx = __shfl(g, qb);
         const float gx = __shfl(g, qb + 1), gy = __shfl(g, qb + 2), gz = __shfl(g, qb + 3);
         float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
@@ -709,7 +718,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         ny = ny * im;
         nz = nz * im;
         if (valid && j == 0) {
-            const uint32_t gi = p.voff[R.w] + (R.vidKey & 0xffffu);
+            const uint32_t gi = outBase + (R.vidKey & 0xffffu);
             p.pos[gi * 3 + 0] = P0; p.pos[gi * 3 + 1] = P1; p.pos[gi * 3 + 2] = P2;
             p.nrm[gi * 3 + 0] = nx; p.nrm[gi * 3 + 1] = ny; p.nrm[gi * 3 + 2] = nz;
             p.col[gi * 3 + 0] = colr[0]; p.col[gi * 3 + 1] = colr[1]; p.col[gi * 3 + 2] = colr[2];

@@ -598,7 +598,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     const char* cullEnv = getenv("PSGPU_CULL");
     if (cullEnv) c->cull = atoi(cullEnv) != 0;
     const char* jitEnv = getenv("PSGPU_JIT");
-    if (jitEnv) c->useJit = atoi(jitEnv) != 0;
+    if (jitEnv) c->useJit = std::min(2, std::max(0, atoi(jitEnv)));
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -625,10 +625,11 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
     else if (option == PSGPU_OPT_JIT) {
-        c->useJit = value != 0;
+        if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
+        c->useJit = (int)value;
         if (!c->useJit) c->jit.reset();
         else if (c->haveModel) {
-            c->jit = jit_get(c->model, c->device, &c->jitError);
+            c->jit = jit_get(c->model, c->useJit == 2, c->device, &c->jitError);
             if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
         }
     }
@@ -653,7 +654,7 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     c->haveModel = true;
     c->jit.reset();
     if (c->useJit) {
-        c->jit = jit_get(c->model, c->device, &c->jitError);
+        c->jit = jit_get(c->model, c->useJit == 2, c->device, &c->jitError);
         if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
     }
     return PSGPU_RET_SUCCESS;
@@ -879,13 +880,13 @@ int psgpu_field_values(psgpu_ctx* c, const float* xyz, uint32_t n, int mode, flo
 // Host-only: build the device image of a model and compile its specialised kernels
 // (no GPU needed).  Returns the code-object size, or a negative error code.
 long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats, const PsSoaBlobOps* ops,
-                       char* log, size_t cap) {
+                       int mode, char* log, size_t cap) {
     if (!prims || !mats || !ops) return PSGPU_RET_PARAM_ERROR;
     std::unique_ptr<DevModel> m(new DevModel);
     int rc = build_device_model(*prims, *mats, *ops, *m);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     std::string err;
-    long n = jit_compile_only(*m, &err);
+    long n = jit_compile_only(*m, mode == 2, &err);
     if (log && cap) {
         const size_t k = std::min(cap - 1, err.size());
         memcpy(log, err.data(), k);
@@ -900,7 +901,7 @@ int psgpu_jit_active(psgpu_ctx* c) { return c && c->jit ? 1 : 0; }
 // Generated specialised source for the current model (NUL-terminated, truncated to cap).
 int psgpu_jit_source(psgpu_ctx* c, char* buf, size_t cap) {
     if (!c || !c->haveModel) return PSGPU_RET_PARAM_ERROR;
-    const std::string s = jit_source(c->model);
+    const std::string s = jit_source(c->model, c->useJit == 2);
     if (buf && cap) {
         const size_t n = std::min(cap - 1, s.size());
         memcpy(buf, s.data(), n);

@@ -15,10 +15,11 @@ struct JitKernels {
 };
 
 // Compiled (cached per structure and device) kernels for the model; nullptr + *err on failure.
-std::shared_ptr<JitKernels> jit_get(const DevModel& m, int device, std::string* err);
+// baked: primitive / op parameters compiled in as literals (recompiles when they change).
+std::shared_ptr<JitKernels> jit_get(const DevModel& m, bool baked, int device, std::string* err);
 // Compile (and cache) without loading: code-object size, or -1 and *err.  No GPU needed.
-long jit_compile_only(const DevModel& m, std::string* err);
+long jit_compile_only(const DevModel& m, bool baked, std::string* err);
 // The generated HIP source (tests and debugging).
-std::string jit_source(const DevModel& m);
+std::string jit_source(const DevModel& m, bool baked);
 
 }  // namespace psgpu

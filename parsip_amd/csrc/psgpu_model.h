@@ -109,9 +109,11 @@ struct DevModel {
 };
 
 // Compact-mesh work records written by the MPU kernel.
-struct VertexRec {       // 8 B: surface-MPU slot, local vertex id, edge key
+struct VertexRec {       // 16 B: surface-MPU slot, global MPU id, local vertex id, edge key
     uint32_t w;
+    uint32_t m;
     uint32_t vidKey;     // vid | key << 16, key = sx | sy<<3 | sz<<6 | axis<<9
+    uint32_t pad;
 };
 struct TriRec {          // 16 B
     uint32_t w;

@@ -84,7 +84,7 @@ def load(build_if_missing: bool = True):
         "psgpu_set_option": ([vp, i32, ctypes.c_int64], i32),
         "psgpu_jit_active": ([vp], i32),
         "psgpu_jit_source": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
-        "psgpu_jit_compile": ([vp, vp, vp, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
+        "psgpu_jit_compile": ([vp, vp, vp, i32, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -127,10 +127,10 @@ def tritable() -> np.ndarray:
     return t
 
 
-def jit_compile(model: soa.Model) -> int:
+def jit_compile(model: soa.Model, mode: int = 1) -> int:
     """Host-only: compile the model's specialised kernels (hiprtc); returns code size."""
     log = ctypes.create_string_buffer(1 << 16)
-    n = load().psgpu_jit_compile(*model.ptrs(), log, len(log))
+    n = load().psgpu_jit_compile(*model.ptrs(), mode, log, len(log))
     if n < 0:
         raise PsgpuError(n, "psgpu_jit_compile: " + log.value.decode(errors="replace"))
     return n
