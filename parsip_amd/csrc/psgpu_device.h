@@ -434,6 +434,13 @@ struct InterpEval {
         }
         return noOps ? acc : last;
     }
+
+    template <int GROUP, bool COLOR, int N>
+    __device__ __forceinline__ void evaln(const float* px, const float* py, const float* pz, const CullMask& cm,
+                                          float* out, float* colOut) const {
+        for (int n = 0; n < N; ++n)
+            out[n] = eval<GROUP, COLOR>(px[n], py[n], pz[n], cm, COLOR ? colOut + 3 * n : nullptr);
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -479,6 +486,9 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds, uint3
 // Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
 // LDS per wave: fv[512] f32 | edgeVid[1536] u16 | cfg[344] u8 | vbase[344] u16 |
 //               tbase[344] u16 | value slots (interpreter only)
+#ifndef PSGPU_S2_N
+#define PSGPU_S2_N 8  // x-slices per walk in S2 (1, 2, 4 or 8)
+#endif
 constexpr int kLdsFv = 0;
 constexpr int kLdsEdge = 2048;
 constexpr int kLdsCfg = kLdsEdge + 1536 * 2;
@@ -526,12 +536,22 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         const float e = 7.0f * cs;
         cm = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
     }
-    uint32_t inside = 0;
+    // all 8 x-slices of this lane's (y,z) needle in one walk (EV::evaln, N = 8)
+    float pxs[8], pys[8], pzs[8], fs8[8];
+#pragma unroll
     for (int x = 0; x < 8; ++x) {
-        const float px = o[0] + (float)x * cs;
-        const float f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
-        fv[x * 64 + lane] = f;
-        inside += __popcll(ballot(f >= 0.5f));
+        pxs[x] = o[0] + (float)x * cs;
+        pys[x] = py;
+        pzs[x] = pz;
+    }
+#pragma unroll
+    for (int h = 0; h < 8; h += PSGPU_S2_N)
+        ev.template evaln<4, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs8 + h, nullptr);
+    uint32_t inside = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+        fv[x * 64 + lane] = fs8[x];
+        inside += __popcll(ballot(fs8[x] >= 0.5f));
     }
     if (inside == 0 || inside == 512) {
         if (lane == 0) p.counts[w] = make_uint2(0u, 0u);
