@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
                     help="0 interpreter, 1 kernels specialised per tree structure, 2 + parameters baked in")
+    ap.add_argument("--debug", type=int, default=0, help=argparse.SUPPRESS)  # profiling ablations only
     args = ap.parse_args()
 
     grp = Group()
@@ -118,6 +119,8 @@ def main():
     if args.no_cull:
         poly.set_option(gpu.OPT_CULLING, 0)
     poly.set_option(gpu.OPT_JIT, args.jit)
+    if args.debug:
+        poly.set_option(gpu.OPT_DEBUG, args.debug)
 
     frame = grp.rank if args.scaling == "weak" else 0
     model, cs, N = synth.make_config(args.config, frame=frame)

@@ -148,7 +148,7 @@ typedef struct PsMeshInfo {
 
 /* Device-resident compact mesh of the last polygonization (pointers into the
  * context's HBM buffers; valid until the next psgpu_polygonize on the context).
- * Vertices of MPU w occupy [mpuVertexOffset[w], mpuVertexOffset[w]+ct) in MPU order,
+ * Vertices of slot w occupy [(uint32)mpuOffsets[w], (uint32)mpuOffsets[w+1]) in MPU order,
  * i.e. exactly the reference's concatenation of vMPUs[i].vPos over i.              */
 typedef struct PsMeshDevice {
     const float*    pos;              /* ctVertices * 3, xyz interleaved           */
@@ -156,8 +156,8 @@ typedef struct PsMeshDevice {
     const float*    col;              /* ctVertices * 3                            */
     const uint32_t* tris;             /* ctTriangles * 3, global vertex ids        */
     const uint32_t* surfaceMpuIds;    /* ctPassedPrecheck: global MPU id per slot  */
-    const uint32_t* mpuVertexOffset;  /* ctPassedPrecheck + 1 (exclusive scan)     */
-    const uint32_t* mpuTriangleOffset;/* ctPassedPrecheck + 1                      */
+    const uint64_t* mpuOffsets;       /* ctPassedPrecheck + 1, exclusive scan:
+                                         vertexOffset | triangleOffset << 32      */
 } PsMeshDevice;
 
 typedef struct psgpu_ctx psgpu_ctx;
@@ -216,6 +216,7 @@ int  psgpu_field_values(psgpu_ctx* ctx, const float* xyz, uint32_t n, int mode, 
 int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_KERNEL_TIMING 1   /* 1: record hipEvents around every kernel */
 #define PSGPU_OPT_CULLING       2   /* 1: exact per-wave primitive culling (default) */
+#define PSGPU_OPT_DEBUG         9   /* profiling ablations (bit 0: stop after S2); 0 in use */
 #define PSGPU_OPT_JIT           3   /* 0 interpreter, 1 specialised per structure (default),
                                        2 specialised with parameters baked in */
 /* Host-only (no GPU): compile the model's specialised kernels with hiprtc (mode 1:

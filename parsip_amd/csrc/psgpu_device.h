@@ -456,7 +456,7 @@ __device__ __forceinline__ void mpu_origin(const Params& p, uint32_t m, float o[
 // S1: 8 corners per MPU, lanes 0-3 z = lo, lanes 4-7 z = lo + side; (x,y) lanes
 // (0,0),(1,0),(0,1),(1,1) (PS_Polygonizer.cpp:488-519).  256 threads = 32 MPUs.
 template <class EV>
-__device__ __forceinline__ void precheck_body(const Params& p, float* lds, uint32_t* waveMask) {
+__device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane_id());
     const uint32_t local = (blockIdx.x * 256 + threadIdx.x) >> 3;
@@ -472,22 +472,16 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds, uint3
     const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
     const float f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
     const uint64_t b = ballot(valid && f > 0.0f);
-    if (lane_id() == 0) {
-        uint32_t mk = 0;
+    if (lane_id() == 0) {  // one flag byte per MPU: 8 MPUs per wave, one 8-byte store
+        uint64_t flags = 0;
 #pragma unroll
-        for (int g = 0; g < 8; ++g) mk |= (((b >> (8 * g)) & 0xffull) != 0ull ? 1u : 0u) << g;
-        waveMask[wave] = mk;
+        for (int g = 0; g < 8; ++g) flags |= (((b >> (8 * g)) & 0xffull) != 0ull ? 1ull : 0ull) << (8 * g);
+        reinterpret_cast<uint64_t*>(p.passFlags)[blockIdx.x * 4 + wave] = flags;
     }
-    __syncthreads();
-    if (threadIdx.x == 0)
-        p.passMask[blockIdx.x] = waveMask[0] | (waveMask[1] << 8) | (waveMask[2] << 16) | (waveMask[3] << 24);
 }
 
-// Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
-// LDS per wave: fv[512] f32 | edgeVid[1536] u16 | cfg[344] u8 | vbase[344] u16 |
-//               tbase[344] u16 | value slots (interpreter only)
 #ifndef PSGPU_S2_N
-#define PSGPU_S2_N 8  // x-slices per walk in S2 (1, 2, 4 or 8)
+#define PSGPU_S2_N 1  // x-slices per walk in S2 (1, 2, 4 or 8)
 #endif
 constexpr int kLdsFv = 0;
 constexpr int kLdsEdge = 2048;
@@ -496,30 +490,33 @@ constexpr int kLdsVbase = kLdsCfg + 344;
 constexpr int kLdsTbase = kLdsVbase + 344 * 2;
 constexpr int kLdsSlots = ((kLdsTbase + 344 * 2) + 15) & ~15;
 
-// owner cell of an edge = the first cell in (i,j,k) order that lists it (every cell
-// containing a sign-changing edge lists it: SURVEY.md §8(a) a9)
-__device__ __forceinline__ bool owns_edge(int i, int j, int k, int sx, int sy, int sz, int ax) {
-    const int ox = ax == 0 ? sx : max(sx - 1, 0);
-    const int oy = ax == 1 ? sy : max(sy - 1, 0);
-    const int oz = ax == 2 ? sz : max(sz - 1, 0);
-    return ox == i && oy == j && oz == k;
-}
+// Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
+// LDS per block: the packed cube tables (shared), then per wave: fv[512] f32 |
+// edgeVid[1536] u16 | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots.
+constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
 
 template <class EV>
 __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
+    // stage the tables in LDS (every wave of the block takes part before any exits)
+    CubeTablesDev* tab = reinterpret_cast<CubeTablesDev*>(smem);
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tables);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+        for (int i = threadIdx.x; i < (int)(sizeof(CubeTablesDev) / 4); i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
     const uint32_t w = blockIdx.x * 4 + wave;
     const uint32_t passCount = p.ctr->passCount;
     if (w >= passCount) return;
-    unsigned char* base = smem + wave * (kLdsSlots + p.slotsPerLane * 64 * 4);
+    unsigned char* base = smem + kLdsTables + wave * (kLdsSlots + p.slotsPerLane * 64 * 4);
     float* fv = reinterpret_cast<float*>(base + kLdsFv);
     uint16_t* edgeVid = reinterpret_cast<uint16_t*>(base + kLdsEdge);
     uint8_t* cellCfg = base + kLdsCfg;
     uint16_t* cellV = reinterpret_cast<uint16_t*>(base + kLdsVbase);
     uint16_t* cellT = reinterpret_cast<uint16_t*>(base + kLdsTbase);
     ModelPtr M = as_const(p.model);
-    TablePtr tab = as_const(p.tables);
     EV ev(M, reinterpret_cast<float*>(base + kLdsSlots) + lane);
 
     const uint32_t m = __builtin_amdgcn_readfirstlane(p.passList[w]);
@@ -536,7 +533,6 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         const float e = 7.0f * cs;
         cm = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
     }
-    // all 8 x-slices of this lane's (y,z) needle in one walk (EV::evaln, N = 8)
     float pxs[8], pys[8], pzs[8], fs8[8];
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
@@ -544,23 +540,30 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         pys[x] = py;
         pzs[x] = pz;
     }
+#if PSGPU_S2_N == 1
+    // one walk per x-slice in a runtime loop: the walk's code stays resident in the
+    // instruction cache (unrolled copies of a 32-primitive walk do not fit)
+#pragma unroll 1
+    for (int h = 0; h < 8; ++h) fs8[h] = ev.template eval<4, false>(pxs[h], py, pz, cm, nullptr);
+#else
 #pragma unroll
     for (int h = 0; h < 8; h += PSGPU_S2_N)
         ev.template evaln<4, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs8 + h, nullptr);
+#endif
     uint32_t inside = 0;
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
         fv[x * 64 + lane] = fs8[x];
         inside += __popcll(ballot(fs8[x] >= 0.5f));
     }
-    if (inside == 0 || inside == 512) {
-        if (lane == 0) p.counts[w] = make_uint2(0u, 0u);
-        return;
-    }
+    if (inside == 0 || inside == 512 || (p.debug & 1u)) return;  // counts stay zero
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
-    // S3 pass 1: configs, owned (new) vertices and triangles per cell, wave scans
+    // S3 pass 1 (:647-691): config per cell (bit c = x*4 + y*2 + z, inside = f >= 0.5),
+    // owned sign-changing edges (new vertices) and triangles; wave prefix sums give
+    // the reference's discovery order over cells (i,j,k)
+    const uint64_t edgeBits = tab->edge;
     uint32_t carryV = 0, carryT = 0;
     for (int q = 0; q < 6; ++q) {
         const int c = q * 64 + lane;
@@ -575,15 +578,8 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         }
         uint32_t nv = 0, nt = 0;
         if (cfg != 0 && cfg != 255) {
-            uint32_t seen = 0;
-            for (int e = 0; e < 16; ++e) {
-                const int ed = tab->tri[cfg][e];
-                if (ed < 0) break;
-                if ((seen >> ed) & 1u) continue;
-                seen |= 1u << ed;
-                const int c1 = tab->corner1[ed], ax = tab->axis[ed];
-                nv += owns_edge(i, j, k, i + ((c1 >> 2) & 1), j + ((c1 >> 1) & 1), k + (c1 & 1), ax) ? 1u : 0u;
-            }
+            const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
+            nv = __popc(own & tab->cross[cfg]);
             nt = tab->ntri[cfg];
         }
         const uint32_t sv = wave_incl_scan(nv);
@@ -597,44 +593,50 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         carryT += __shfl(st, 63);
     }
     const uint32_t V = carryV, T = carryT;
+    const uint32_t shard = w & (kShards - 1);
     uint32_t qv = 0, qt = 0;
     if (lane == 0) {
-        qv = atomicAdd(&p.ctr->vCount, V);
-        qt = atomicAdd(&p.ctr->tCount, T);
-        p.counts[w] = make_uint2(V, T);
+        qv = atomicAdd(&p.ctr->vShard[shard], V);
+        qt = atomicAdd(&p.ctr->tShard[shard], T);
+        p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
+        if (T > 0) atomicAdd(&p.ctr->sShard[shard], 1u);
+        if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
     }
     qv = __shfl(qv, 0);
     qt = __shfl(qt, 0);
+    VertexRec* vq = p.vq + (size_t)shard * p.vShardCap;
+    TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if (p.debug & 2u) return;  // ablation: pass 1 only
 
-    // pass 2: vertex ids in the reference's discovery order, vertex records
+    // pass 2 (:703-808): vertex ids in first-occurrence order of the row, records
     for (int q = 0; q < 6; ++q) {
         const int c = q * 64 + lane;
         if (c >= 343) break;
         const uint32_t cfg = cellCfg[c];
         if (cfg == 0 || cfg == 255) continue;
         const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+        const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
+        const uint64_t order = tab->order[cfg];
+        const int nd = __popc(tab->cross[cfg]);
         uint32_t vid = cellV[c];
-        uint32_t seen = 0;
-        for (int e = 0; e < 16; ++e) {
-            const int ed = tab->tri[cfg][e];
-            if (ed < 0) break;
-            if ((seen >> ed) & 1u) continue;
-            seen |= 1u << ed;
-            const int c1 = tab->corner1[ed], ax = tab->axis[ed];
+        for (int r = 0; r < nd; ++r) {
+            const int ed = (int)((order >> (4 * r)) & 15u);
+            if (!((own >> ed) & 1u)) continue;
+            const int eb = (int)((edgeBits >> (5 * ed)) & 31u);
+            const int c1 = eb & 7, ax = eb >> 3;
             const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
-            if (owns_edge(i, j, k, sx, sy, sz, ax)) {
-                edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)vid;
-                const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
-                const uint32_t g = qv + vid;
-                if (g < p.vcap) p.vq[g] = VertexRec{w, m, vid | (key << 16), 0u};
-                ++vid;
-            }
+            edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)vid;
+            const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
+            const uint32_t g = qv + vid;
+            if (g < p.vShardCap) vq[g] = VertexRec{w, m, vid | (key << 16), 0u};
+            ++vid;
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if (p.debug & 4u) return;  // ablation: no triangles
 
     // pass 3 (S6, :816-825): triangles in table order
     for (int q = 0; q < 6; ++q) {
@@ -645,20 +647,44 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         const int i = c / 49, j = (c / 7) % 7, k = c % 7;
         const uint32_t tb = cellT[c];
         const uint32_t nt = tab->ntri[cfg];
+        const uint64_t row = tab->row[cfg];
         for (uint32_t t = 0; t < nt; ++t) {
             uint32_t v[3];
 #pragma unroll
             for (int s = 0; s < 3; ++s) {
-                const int ed = tab->tri[cfg][t * 3 + s];
-                const int c1 = tab->corner1[ed], ax = tab->axis[ed];
+                const int ed = (int)((row >> (4 * (t * 3 + s))) & 15u);
+                const int eb = (int)((edgeBits >> (5 * ed)) & 31u);
+                const int c1 = eb & 7, ax = eb >> 3;
                 const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
                 v[s] = edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax];
             }
             const uint32_t g = qt + tb + t;
-            if (g < p.tcap) p.tq[g] = TriRec{w, tb + t, v[0] | (v[1] << 16), v[2]};
+            if (g < p.tShardCap) tq[g] = TriRec{w, tb + t, v[0] | (v[1] << 16), v[2]};
         }
     }
 }
+
+// Batches of `per` records over the kShards queues: lane l holds shard l's batch
+// count, so a batch index maps to (shard, first record) with one ballot.
+struct ShardBatches {
+    uint32_t cnt, incl, total;
+    __device__ ShardBatches(const uint32_t* counts, uint32_t cap, uint32_t per) {
+        cnt = min(counts[lane_id()], cap);
+        const uint32_t nb = (cnt + per - 1) / per;
+        incl = wave_incl_scan(nb);
+        total = __shfl(incl, kShards - 1);
+        perBatch = per;
+        nbat = nb;
+    }
+    uint32_t perBatch, nbat;
+    __device__ void locate(uint32_t b, uint32_t* shard, uint32_t* first, uint32_t* count) const {
+        const uint32_t s = (uint32_t)__popcll(ballot(incl <= b));
+        const uint32_t start = __shfl(incl - nbat, (int)s);
+        *shard = s;
+        *first = (b - start) * perBatch;
+        *count = __shfl(cnt, (int)s);
+    }
+};
 
 // Vertices: batches of 16 vertices per wavefront iteration, one quad per vertex.
 // Phase A (quad pruning): the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762)
@@ -670,21 +696,22 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
-    const uint32_t nV = min(p.ctr->vCount, p.vcap);
-    const int j = lane & 3;
     const float third = 1.0f / 3.0f;
+    const int j = lane & 3;
     const float r = (float)j * third;
     const float delta = 0.001f;
     const float inv = -1.0f / delta;
+    const ShardBatches sb(p.ctr->vShard, p.vShardCap, 16);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave;; batch += nWaves) {
-        const uint32_t v0 = batch * 16;
-        if (v0 >= nV) break;
-        uint32_t rec = v0 + (lane >> 2);
-        const bool valid = rec < nV;
-        if (!valid) rec = v0;
+    for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sb.locate(batch, &shard, &first, &count);
+        uint32_t rec = first + (lane >> 2);
+        const bool valid = rec < count;
+        if (!valid) rec = first;
+        rec += shard * p.vShardCap;
         const VertexRec R = p.vq[rec];
-        const uint32_t outBase = p.voff[R.w];  // consumed at the end: latency overlaps the walk
+        const uint32_t outBase = (uint32_t)p.offs[R.w];  // consumed at the end: latency overlaps the walk
         const uint32_t m = R.m;
         float o[3];
         mpu_origin(p, m, o);

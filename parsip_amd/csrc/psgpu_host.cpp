@@ -87,6 +87,48 @@ const CubeTables& cube_tables() {
     return T;
 }
 
+// Packed device tables (psgpu_model.h CubeTablesDev).
+void fill_device_tables(const CubeTables& T, CubeTablesDev& D) {
+    memset(&D, 0, sizeof(D));
+    for (int c = 0; c < 256; ++c) {
+        uint64_t row = 0, order = 0;
+        uint32_t seen = 0;
+        int nd = 0;
+        for (int e = 0; e < 16 && T.tri[c][e] >= 0; ++e) {
+            const int ed = T.tri[c][e];
+            row |= (uint64_t)ed << (4 * e);
+            if (!((seen >> ed) & 1u)) {
+                seen |= 1u << ed;
+                order |= (uint64_t)ed << (4 * nd++);
+            }
+        }
+        uint32_t cross = 0;
+        for (int e = 0; e < 12; ++e)
+            if (((c >> T.corner1[e]) & 1) != ((c >> T.corner2[e]) & 1)) cross |= 1u << e;
+        D.row[c] = row;
+        D.order[c] = order;
+        D.cross[c] = (uint16_t)cross;
+        D.ntri[c] = T.ntri[c];
+    }
+    // ownership: the first cell in (i,j,k) order containing an edge owns it; an edge
+    // starting at cell corner (cx,cy,cz) on axis a is owned by this cell iff every
+    // non-axis corner bit is 1 or the cell sits on that axis' low boundary
+    for (int b = 0; b < 8; ++b) {
+        const bool i0 = b & 4, j0 = b & 2, k0 = b & 1;
+        uint32_t m = 0;
+        for (int e = 0; e < 12; ++e) {
+            const int c1 = T.corner1[e], ax = T.axis[e];
+            const bool bx = (c1 >> 2) & 1, by = (c1 >> 1) & 1, bz = c1 & 1;
+            const bool okx = ax == 0 || bx || i0, oky = ax == 1 || by || j0, okz = ax == 2 || bz || k0;
+            if (okx && oky && okz) m |= 1u << e;
+        }
+        D.own[b] = (uint16_t)m;
+    }
+    uint64_t edge = 0;
+    for (int e = 0; e < 12; ++e) edge |= (uint64_t)(T.corner1[e] | (T.axis[e] << 3)) << (5 * e);
+    D.edge = edge;
+}
+
 // ---------------------------------------------------------------------------
 // Walk program: the reference's processing order of fieldValue's explicit stack.
 bool op_needs_left(int t) { return (t >= 14 && t <= 19) || (t >= 22 && t <= 25); }
@@ -259,7 +301,7 @@ hipError_t grow(T*& ptr, size_t& cap, size_t need) {
 }
 
 constexpr int kNumKernels = 6;
-const char* kKernelNames[kNumKernels] = {"k_precheck", "k_compact", "k_mpu", "k_scan", "k_vertex", "k_tris"};
+const char* kKernelNames[kNumKernels] = {"k_precheck", "select", "k_mpu", "scan", "k_vertex", "k_tris"};
 
 }  // namespace
 
@@ -276,6 +318,7 @@ struct psgpu_ctx {
     std::string jitError;
     bool haveModel = false;
     int cull = 1;
+    int debug = 0;
     int timing = 0;
     // geometry of the last run
     float cs = 0.0f;
@@ -285,12 +328,13 @@ struct psgpu_ctx {
     bool pending = false;
     bool haveResult = false;
     // device buffers
-    size_t capMask = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
-    uint32_t* passMask = nullptr;
+    size_t capFlags = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
+    size_t capTemp = 0;
+    uint8_t* passFlags = nullptr;
     uint32_t* passList = nullptr;
-    uint2* counts = nullptr;
-    uint32_t* voff = nullptr;
-    uint32_t* toff = nullptr;
+    uint64_t* counts = nullptr;
+    uint64_t* offs = nullptr;
+    unsigned char* temp = nullptr;  // rocPRIM scratch
     VertexRec* vq = nullptr;
     TriRec* tq = nullptr;
     float* pos = nullptr;
@@ -301,7 +345,8 @@ struct psgpu_ctx {
     uint32_t* dequeue = nullptr;
     DevCounters* hostCtr = nullptr;  // pinned
     DevCounters* initCtr = nullptr;  // pinned template
-    uint32_t vcap = 1u << 20, tcap = 1u << 21;
+    uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
+    uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
     hipEvent_t ev[kNumKernels + 1] = {};
     float lastMs[kNumKernels] = {};
     PsMeshInfo info{};
@@ -323,14 +368,16 @@ int hip_fail(hipError_t e, const char* what) {
 
 int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     const size_t n = std::max<uint32_t>(mpuCount, 1);
-    PSGPU_CHECK(grow(c->passMask, c->capMask, (n + 31) / 32));
+    PSGPU_CHECK(grow(c->passFlags, c->capFlags, (n + 31) / 32 * 32));
     PSGPU_CHECK(grow(c->passList, c->capList, n));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
-    size_t capOff2 = c->capOff;
-    PSGPU_CHECK(grow(c->voff, c->capOff, n + 1));
-    PSGPU_CHECK(grow(c->toff, capOff2, n + 1));
-    PSGPU_CHECK(grow(c->vq, c->capVq, c->vcap));
-    PSGPU_CHECK(grow(c->tq, c->capTq, c->tcap));
+    PSGPU_CHECK(grow(c->offs, c->capOff, n + 1));
+    size_t b1 = 0, b2 = 0;
+    PSGPU_CHECK(select_passing(nullptr, b1, c->passFlags, 0, c->passList, &c->ctr->passCount, (uint32_t)n, c->stream));
+    PSGPU_CHECK(scan_counts(nullptr, b2, c->counts, c->offs, (uint32_t)n, c->stream));
+    PSGPU_CHECK(grow(c->temp, c->capTemp, std::max(b1, b2) + 256));
+    PSGPU_CHECK(grow(c->vq, c->capVq, (size_t)c->vShardCap * kShards));
+    PSGPU_CHECK(grow(c->tq, c->capTq, (size_t)c->tShardCap * kShards));
     size_t capV2 = c->capV, capV3 = c->capV;
     PSGPU_CHECK(grow(c->pos, c->capV, (size_t)c->vcap * 3));
     PSGPU_CHECK(grow(c->nrm, capV2, (size_t)c->vcap * 3));
@@ -352,15 +399,14 @@ Params make_params(psgpu_ctx* c) {
     p.mpuBegin = c->mpuBegin;
     p.mpuCount = c->mpuCount;
     p.cull = (uint32_t)c->cull;
-    p.passMask = c->passMask;
+    p.passFlags = c->passFlags;
     p.passList = c->passList;
     p.counts = c->counts;
-    p.voff = c->voff;
-    p.toff = c->toff;
+    p.offs = c->offs;
     p.vq = c->vq;
-    p.vcap = c->vcap;
+    p.vShardCap = c->vShardCap;
     p.tq = c->tq;
-    p.tcap = c->tcap;
+    p.tShardCap = c->tShardCap;
     p.pos = c->pos;
     p.nrm = c->nrm;
     p.col = c->col;
@@ -368,6 +414,7 @@ Params make_params(psgpu_ctx* c) {
     p.ctr = c->ctr;
     p.dequeue = c->dequeue;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
+    p.debug = (uint32_t)c->debug;
     return p;
 }
 
@@ -380,6 +427,10 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     Params p = make_params(c);
     PSGPU_CHECK(hipMemcpyAsync(c->ctr, c->initCtr, sizeof(DevCounters), hipMemcpyHostToDevice, s));
     PSGPU_CHECK(hipMemsetAsync(c->dequeue, 0, 4 * sizeof(uint32_t), s));
+    if (c->mpuCount > 0) {
+        PSGPU_CHECK(hipMemsetAsync(c->counts, 0, (size_t)c->mpuCount * sizeof(uint64_t), s));
+        PSGPU_CHECK(hipMemsetAsync(c->offs, 0, sizeof(uint64_t), s));
+    }
     const bool t = c->timing != 0;
     const uint32_t persist = (uint32_t)c->numCUs * 4;
     JitKernels* J = c->jit.get();
@@ -388,12 +439,15 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         if (J) PSGPU_CHECK(launch_jit(J->precheck, (p.mpuCount + 31) / 32, 256, 0, s, p));
         else PSGPU_CHECK(launch_precheck(p, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-        PSGPU_CHECK(launch_compact(p, s));
+        size_t tb = c->capTemp;
+        PSGPU_CHECK(select_passing(c->temp, tb, c->passFlags, c->mpuBegin, c->passList, &c->ctr->passCount,
+                                   c->mpuCount, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
         if (J) PSGPU_CHECK(launch_jit(J->mpu, (p.mpuCount + 3) / 4, 256, mpu_lds_bytes(0), s, p));
         else PSGPU_CHECK(launch_mpu(p, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-        PSGPU_CHECK(launch_scan(p, s));
+        tb = c->capTemp;
+        PSGPU_CHECK(scan_counts(c->temp, tb, c->counts, c->offs, c->mpuCount, s));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
         if (J) PSGPU_CHECK(launch_jit(J->vertex, persist, 256, 0, s, p));
         else PSGPU_CHECK(launch_vertex(p, s, persist));
@@ -577,10 +631,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
         c->numCUs = prop.multiProcessorCount;
     const CubeTables& T = cube_tables();
     CubeTablesDev tabHost{};
-    memcpy(tabHost.tri, T.tri, sizeof(tabHost.tri));
-    memcpy(tabHost.ntri, T.ntri, sizeof(tabHost.ntri));
-    memcpy(tabHost.corner1, T.corner1, sizeof(tabHost.corner1));
-    memcpy(tabHost.axis, T.axis, sizeof(tabHost.axis));
+    fill_device_tables(T, tabHost);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->dTables, sizeof(CubeTablesDev)) != hipSuccess ||
         hipMemcpy(c->dTables, &tabHost, sizeof(CubeTablesDev), hipMemcpyHostToDevice) != hipSuccess ||
@@ -608,7 +659,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->jit.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->passMask, c->passList, c->counts, c->voff, c->toff, c->vq, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->passFlags, c->passList, c->counts, c->offs, c->temp, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->dequeue};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -624,6 +675,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (!c) return PSGPU_RET_PARAM_ERROR;
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
+    else if (option == PSGPU_OPT_DEBUG) c->debug = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;
@@ -691,12 +743,21 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         if (rc != PSGPU_RET_SUCCESS) return rc;
         PSGPU_CHECK(hipStreamSynchronize(c->runStream));
         c->pending = false;
-        // grow and re-run if the compact outputs did not fit
+        // grow and re-run if the work queues or the compact outputs did not fit
         for (int attempt = 0; attempt < 4; ++attempt) {
-            const DevCounters h = *c->hostCtr;
-            if (h.vCount <= c->vcap && h.tCount <= c->tcap) break;
-            c->vcap = std::max(c->vcap, h.vCount + h.vCount / 8 + 1024);
-            c->tcap = std::max(c->tcap, h.tCount + h.tCount / 8 + 1024);
+            const DevCounters& h = *c->hostCtr;
+            uint32_t V = 0, T = 0, mv = 0, mt = 0;
+            for (int k = 0; k < kShards; ++k) {
+                V += h.vShard[k];
+                T += h.tShard[k];
+                mv = std::max(mv, h.vShard[k]);
+                mt = std::max(mt, h.tShard[k]);
+            }
+            if (V <= c->vcap && T <= c->tcap && mv <= c->vShardCap && mt <= c->tShardCap) break;
+            c->vcap = std::max(c->vcap, V + V / 8 + 1024);
+            c->tcap = std::max(c->tcap, T + T / 8 + 1024);
+            c->vShardCap = std::max(c->vShardCap, mv + mv / 4 + 256);
+            c->tShardCap = std::max(c->tShardCap, mt + mt / 4 + 256);
             rc = ensure_buffers(c, c->mpuCount);
             if (rc != PSGPU_RET_SUCCESS) return rc;
             rc = enqueue(c, c->runStream);
@@ -709,14 +770,20 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
                 if (hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]) == hipSuccess) c->lastMs[k] = ms;
             }
         }
-        const DevCounters h = *c->hostCtr;
+        const DevCounters& h = *c->hostCtr;
+        uint32_t V = 0, T = 0, S = 0;
+        for (int k = 0; k < kShards; ++k) {
+            V += h.vShard[k];
+            T += h.tShard[k];
+            S += h.sShard[k];
+        }
         PsMeshInfo& I = c->info;
         memset(&I, 0, sizeof(I));
         I.ctMPUs = c->mpuCount;
         I.ctPassedPrecheck = c->mpuCount ? h.passCount : 0;
-        I.ctSurfaceMPUs = c->mpuCount ? h.surfaceCount : 0;
-        I.ctVertices = c->mpuCount ? h.vCount : 0;
-        I.ctTriangles = c->mpuCount ? h.tCount : 0;
+        I.ctSurfaceMPUs = c->mpuCount ? S : 0;
+        I.ctVertices = c->mpuCount ? V : 0;
+        I.ctTriangles = c->mpuCount ? T : 0;
         I.firstOverflowMPU = (c->mpuCount && h.firstOverflow != 0x7fffffff) ? h.firstOverflow : -1;
         I.ctLaneEvals = 8ull * c->mpuCount + 512ull * I.ctPassedPrecheck + 8ull * I.ctVertices;
         c->haveResult = true;
@@ -745,8 +812,7 @@ int psgpu_mesh_device(psgpu_ctx* c, PsMeshDevice* out) {
     out->col = c->col;
     out->tris = c->tris;
     out->surfaceMpuIds = c->passList;
-    out->mpuVertexOffset = c->voff;
-    out->mpuTriangleOffset = c->toff;
+    out->mpuOffsets = c->offs;
     return PSGPU_RET_SUCCESS;
 }
 
@@ -761,13 +827,13 @@ int psgpu_download_mesh(psgpu_ctx* c, float* pos, float* nrm, float* col, uint32
     if (col && V) PSGPU_CHECK(hipMemcpy(col, c->col, V * 12, hipMemcpyDeviceToHost));
     if (tris && T) PSGPU_CHECK(hipMemcpy(tris, c->tris, T * 12, hipMemcpyDeviceToHost));
     if (ids && W) PSGPU_CHECK(hipMemcpy(ids, c->passList, W * 4, hipMemcpyDeviceToHost));
-    if (voff) {
-        if (W) PSGPU_CHECK(hipMemcpy(voff, c->voff, (W + 1) * 4, hipMemcpyDeviceToHost));
-        else voff[0] = 0;
-    }
-    if (toff) {
-        if (W) PSGPU_CHECK(hipMemcpy(toff, c->toff, (W + 1) * 4, hipMemcpyDeviceToHost));
-        else toff[0] = 0;
+    if (voff || toff) {
+        std::vector<uint64_t> o(W + 1, 0);
+        if (W) PSGPU_CHECK(hipMemcpy(o.data(), c->offs, (W + 1) * 8, hipMemcpyDeviceToHost));
+        for (size_t w = 0; w <= W; ++w) {
+            if (voff) voff[w] = (uint32_t)o[w];
+            if (toff) toff[w] = (uint32_t)(o[w] >> 32);
+        }
     }
     return PSGPU_RET_SUCCESS;
 }
@@ -777,7 +843,8 @@ int psgpu_download_stats(psgpu_ctx* c, PsMpuStats* stats) {
     int rc = psgpu_finish(c, &I);
     if (rc != PSGPU_RET_SUCCESS || !stats) return rc == PSGPU_RET_SUCCESS ? PSGPU_RET_PARAM_ERROR : rc;
     const uint32_t W = I.ctPassedPrecheck;
-    std::vector<uint32_t> ids(W), cnt(2 * (size_t)W);
+    std::vector<uint32_t> ids(W);
+    std::vector<uint64_t> cnt(W);
     if (W) {
         PSGPU_CHECK(hipMemcpy(ids.data(), c->passList, W * 4, hipMemcpyDeviceToHost));
         PSGPU_CHECK(hipMemcpy(cnt.data(), c->counts, (size_t)W * 8, hipMemcpyDeviceToHost));
@@ -787,8 +854,8 @@ int psgpu_download_stats(psgpu_ctx* c, PsMpuStats* stats) {
         PsMpuStats& s = stats[ids[w] - c->mpuBegin];
         s.passedPrecheck = 1;
         s.ctFieldEvals = 128;
-        s.ctVertices = cnt[2 * w];
-        s.ctTriangles = cnt[2 * w + 1];
+        s.ctVertices = (uint32_t)cnt[w];
+        s.ctTriangles = (uint32_t)(cnt[w] >> 32);
     }
     return PSGPU_RET_SUCCESS;
 }

@@ -4,11 +4,11 @@
 // Polygonize + CMPUProcessor, PS_Polygonizer.cpp:315-385, 441-829):
 //
 //   k_precheck  8 lanes per MPU, 2 quads: S1 corner test F>0          (:483-540)
-//   k_compact   one workgroup: ordered list of MPUs that passed S1
+//   select      rocPRIM: ordered list of MPUs that passed S1 (psgpu_scan.hip)
 //   k_mpu       one wavefront per passing MPU: S2 8^3 field cache in LDS (quads of 4
 //               z-consecutive corners), S3 configs, vertex ownership + wave prefix
 //               sums for the reference's discovery order, triangle records
-//   k_scan      one workgroup: per-MPU vertex/triangle offsets (compact mesh)
+//   scan        rocPRIM: per-MPU vertex/triangle offsets (compact mesh)
 //   k_vertex    one quad per vertex: S4 4-sample root bracket, S5 colour + normals
 //   k_tris      triangle records -> global vertex ids
 //
@@ -25,8 +25,7 @@ namespace psgpu {
 
 __global__ void __launch_bounds__(256) k_precheck(Params p) {
     extern __shared__ float lds[];
-    __shared__ uint32_t waveMask[4];
-    precheck_body<InterpEval>(p, lds, waveMask);
+    precheck_body<InterpEval>(p, lds);
 }
 
 __global__ void __launch_bounds__(256) k_mpu(Params p) {
@@ -45,85 +44,19 @@ __global__ void __launch_bounds__(256) k_probe(Params p, const float* __restrict
     probe_body<InterpEval>(p, plds, xyz, out, colOut, n, mode);
 }
 
-// Ordered compaction of the S1 survivors (single workgroup of 1024 threads).
-__global__ void __launch_bounds__(1024) k_compact(Params p) {
-    __shared__ uint32_t part[1024];
-    const uint32_t nWords = (p.mpuCount + 31) / 32;
-    const uint32_t per = (nWords + 1023) / 1024;
-    const uint32_t w0 = threadIdx.x * per;
-    uint32_t cnt = 0;
-    for (uint32_t w = w0; w < w0 + per && w < nWords; ++w) cnt += __popc(p.passMask[w]);
-    part[threadIdx.x] = cnt;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint32_t v = threadIdx.x >= (uint32_t)off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t base = part[threadIdx.x] - cnt;
-    for (uint32_t w = w0; w < w0 + per && w < nWords; ++w) {
-        uint32_t mk = p.passMask[w];
-        while (mk) {
-            int b = __ffs(mk) - 1;
-            mk &= mk - 1;
-            p.passList[base++] = p.mpuBegin + w * 32 + (uint32_t)b;
-        }
-    }
-    if (threadIdx.x == 1023) p.ctr->passCount = part[1023];
-}
-
-// Exclusive scan of per-MPU (V,T) into mesh offsets (single workgroup).
-__global__ void __launch_bounds__(1024) k_scan(Params p) {
-    __shared__ uint32_t sv[1024], st[1024], surf[1024];
-    const uint32_t n = p.ctr->passCount;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t s0 = threadIdx.x * per;
-    uint32_t a = 0, b = 0, sc = 0;
-    int firstOv = 0x7fffffff;
-    for (uint32_t w = s0; w < s0 + per && w < n; ++w) {
-        const uint2 c = p.counts[w];
-        a += c.x;
-        b += c.y;
-        sc += c.y > 0 ? 1u : 0u;
-        if ((c.x > 512u || c.y > 512u) && firstOv == 0x7fffffff) firstOv = (int)p.passList[w];
-    }
-    if (firstOv != 0x7fffffff) atomicMin(&p.ctr->firstOverflow, firstOv);
-    sv[threadIdx.x] = a;
-    st[threadIdx.x] = b;
-    surf[threadIdx.x] = sc;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint32_t x = threadIdx.x >= (uint32_t)off ? sv[threadIdx.x - off] : 0u;
-        uint32_t y = threadIdx.x >= (uint32_t)off ? st[threadIdx.x - off] : 0u;
-        uint32_t z = threadIdx.x >= (uint32_t)off ? surf[threadIdx.x - off] : 0u;
-        __syncthreads();
-        sv[threadIdx.x] += x;
-        st[threadIdx.x] += y;
-        surf[threadIdx.x] += z;
-        __syncthreads();
-    }
-    uint32_t va = sv[threadIdx.x] - a, ta = st[threadIdx.x] - b;
-    for (uint32_t w = s0; w < s0 + per && w < n; ++w) {
-        const uint2 c = p.counts[w];
-        p.voff[w] = va;
-        p.toff[w] = ta;
-        va += c.x;
-        ta += c.y;
-    }
-    if (threadIdx.x == 1023) {
-        p.voff[n] = sv[1023];
-        p.toff[n] = st[1023];
-        p.ctr->surfaceCount = surf[1023];
-    }
-}
-
 __global__ void __launch_bounds__(256) k_tris(Params p) {
-    const uint32_t nT = min(p.ctr->tCount, p.tcap);
-    for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < nT; t += gridDim.x * 256) {
-        const TriRec R = p.tq[t];
-        const uint32_t g = p.toff[R.w] + R.tlocal;
-        const uint32_t b = p.voff[R.w];
+    const int wave = threadIdx.x >> 6;
+    const ShardBatches sb(p.ctr->tShard, p.tShardCap, 64);
+    const uint32_t nWaves = gridDim.x * 4;
+    for (uint32_t batch = blockIdx.x * 4 + wave; batch < sb.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sb.locate(batch, &shard, &first, &count);
+        const uint32_t t = first + lane_id();
+        if (t >= count) continue;
+        const TriRec R = p.tq[(size_t)shard * p.tShardCap + t];
+        const uint64_t o = p.offs[R.w];
+        const uint32_t g = (uint32_t)(o >> 32) + R.tlocal;
+        const uint32_t b = (uint32_t)o;
         p.tris[g * 3 + 0] = b + (R.v01 & 0xffffu);
         p.tris[g * 3 + 1] = b + (R.v01 >> 16);
         p.tris[g * 3 + 2] = b + R.v2;
@@ -132,7 +65,7 @@ __global__ void __launch_bounds__(256) k_tris(Params p) {
 
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (psgpu_launch.h).
-size_t mpu_lds_bytes(uint32_t slots) { return 4 * (kLdsSlots + (size_t)slots * 64 * 4); }
+size_t mpu_lds_bytes(uint32_t slots) { return kLdsTables + 4 * (kLdsSlots + (size_t)slots * 64 * 4); }
 size_t walk_lds_bytes(uint32_t slots) { return 4 * ((size_t)slots * 4 * 64 * 4); }
 size_t precheck_lds_bytes(uint32_t slots) { return 4 * ((size_t)slots * 64 * 4); }
 
@@ -141,17 +74,9 @@ hipError_t launch_precheck(const Params& p, hipStream_t s) {
     hipLaunchKernelGGL(k_precheck, dim3(blocks), dim3(256), precheck_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
-hipError_t launch_compact(const Params& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, p);
-    return hipGetLastError();
-}
 hipError_t launch_mpu(const Params& p, hipStream_t s) {
     const uint32_t blocks = (p.mpuCount + 3) / 4;
     hipLaunchKernelGGL(k_mpu, dim3(blocks), dim3(256), mpu_lds_bytes(p.slotsPerLane), s, p);
-    return hipGetLastError();
-}
-hipError_t launch_scan(const Params& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks) {

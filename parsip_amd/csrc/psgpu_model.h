@@ -47,12 +47,21 @@ namespace psgpu {
 #define PSGPU_T_BLEND 18
 #define PSGPU_T_RICCI 19
 
-// Marching-cubes tables in device memory (generated on the host, psgpu_host.cpp).
+// Marching-cubes tables in device memory (generated on the host, psgpu_host.cpp),
+// packed so a cell's whole row is one 64-bit word (4 bits per edge id):
+//   row[c]   the triangle row g_triTableCache[c] (<= 15 entries)
+//   order[c] the row's distinct edges in first-occurrence order (<= 12)
+//   cross[c] 12-bit mask of sign-changing edges (== the row's edge set)
+//   ntri[c]  triangles in the row
+//   own[b]   12-bit mask of edges a cell owns, b = (i==0)<<2 | (j==0)<<1 | (k==0)
+//   edge     per edge: corner1 (3 bits) | axis << 3, 5 bits per edge
 struct CubeTablesDev {
-    int8_t tri[256][16];
+    uint64_t row[256];
+    uint64_t order[256];
+    uint16_t cross[256];
     uint8_t ntri[256];
-    uint8_t corner1[12];
-    uint8_t axis[12];
+    uint16_t own[8];
+    uint64_t edge;
     uint8_t pad[8];
 };
 
@@ -123,13 +132,17 @@ struct TriRec {          // 16 B
 };
 
 // Device-side scalars of one polygonization.
+// Work records are appended to kShards independent queues (shard = slot & 63) so that
+// no single counter takes one returning atomic per MPU (a single word saturates at
+// about 88 atomics/us on MI355X: MI355X_MICROARCH.md 'dequeue').
+constexpr int kShards = 64;
 struct DevCounters {
     uint32_t passCount;      // MPUs that passed S1
-    uint32_t vCount;         // vertices reserved
-    uint32_t tCount;         // triangles reserved
-    uint32_t surfaceCount;   // MPUs with >= 1 triangle
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
-    uint32_t pad[3];
+    uint32_t pad[2];
+    uint32_t vShard[kShards];  // vertices appended per shard
+    uint32_t tShard[kShards];  // triangles appended per shard
+    uint32_t sShard[kShards];  // surface MPUs (>= 1 triangle) per shard
 };
 
 // Kernel arguments of one polygonization (one struct, passed by value).
@@ -143,15 +156,14 @@ struct Params {
     uint32_t mpuBegin;
     uint32_t mpuCount;
     uint32_t cull;      // exact per-wave primitive culling enabled
-    uint32_t* passMask;     // ceil(mpuCount/32)
-    uint32_t* passList;     // mpuCount, global MPU ids
-    uint2* counts;          // mpuCount, (V,T) per passing slot
-    uint32_t* voff;         // mpuCount + 1
-    uint32_t* toff;         // mpuCount + 1
-    VertexRec* vq;
-    uint32_t vcap;
-    TriRec* tq;
-    uint32_t tcap;
+    uint8_t* passFlags;     // mpuCount (rounded up to 32): S1 outcome per MPU
+    uint32_t* passList;     // mpuCount, global MPU ids of the S1 survivors, ascending
+    uint64_t* counts;       // mpuCount, V | T << 32 per passing slot (zeroed per run)
+    uint64_t* offs;         // mpuCount + 1, exclusive scan of counts (V | T << 32)
+    VertexRec* vq;          // kShards queues of vShardCap records
+    uint32_t vShardCap;
+    TriRec* tq;             // kShards queues of tShardCap records
+    uint32_t tShardCap;
     float* pos;
     float* nrm;
     float* col;
@@ -159,6 +171,7 @@ struct Params {
     DevCounters* ctr;
     uint32_t* dequeue;      // [2] work counters for k_vertex / k_tris
     uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
+    uint32_t debug;         // ablation switches for profiling (0 in production)
 };
 
 }  // namespace psgpu

@@ -34,8 +34,7 @@ class PsMeshInfo(ctypes.Structure):
 
 
 class PsMeshDevice(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "nrm", "col", "tris", "surfaceMpuIds",
-                                               "mpuVertexOffset", "mpuTriangleOffset")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "nrm", "col", "tris", "surfaceMpuIds", "mpuOffsets")]
 
 
 EXPORTED_SYMBOLS = [
@@ -49,6 +48,7 @@ EXPORTED_SYMBOLS = [
 OPT_KERNEL_TIMING = 1
 OPT_CULLING = 2
 OPT_JIT = 3
+OPT_DEBUG = 9
 
 
 def load(build_if_missing: bool = True):
