@@ -161,7 +161,7 @@ def main():
     evals = costmodel.lane_evals(info.ctMPUs, info.ctPassedPrecheck, info.ctVertices)
     per_eval = costmodel.ops_per_eval(model)
     kernel_evals = {"k_precheck": 8 * info.ctMPUs, "k_mpu": 512 * info.ctPassedPrecheck,
-                    "k_vertex": 8 * info.ctVertices}
+                    "k_vertex": 8 * info.ctVertices, "k_finish": info.ctVertices}
     dom_flops = kernel_evals.get(dom, evals) * per_eval
     achieved = dom_flops / (kt[dom] * 1e-3) / 1e12
     counts = grp.allgather([info.ctVertices, info.ctTriangles])

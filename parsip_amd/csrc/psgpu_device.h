@@ -755,8 +755,9 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         const float qx2 = j == 1 ? P0 + delta : P0;
         const float qy2 = j == 2 ? P1 + delta : P1;
         const float qz2 = j == 3 ? P2 + delta : P2;
-        float colr[3];
-        const float g = ev.template eval<1, true>(qx2, qy2, qz2, cm, colr);
+        // fieldValue at p and at the three normal samples; the colour walk at p runs in
+        // finish_body, 64 vertices per wave (colour work is needed at 1 point in 4)
+        const float g = ev.template eval<1, false>(qx2, qy2, qz2, cm, nullptr);
         const float vtx = __shfl(g, qb);
         const float gx = __shfl(g, qb + 1), gy = __shfl(g, qb + 2), gz = __shfl(g, qb + 3);
         float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
@@ -768,8 +769,49 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             const uint32_t gi = outBase + (R.vidKey & 0xffffu);
             p.pos[gi * 3 + 0] = P0; p.pos[gi * 3 + 1] = P1; p.pos[gi * 3 + 2] = P2;
             p.nrm[gi * 3 + 0] = nx; p.nrm[gi * 3 + 1] = ny; p.nrm[gi * 3 + 2] = nz;
-            p.col[gi * 3 + 0] = colr[0]; p.col[gi * 3 + 1] = colr[1]; p.col[gi * 3 + 2] = colr[2];
         }
+    }
+}
+
+// Finish: vertex colours (fieldValueAndColor's colour walk at every vertex position,
+// PS_Polygonizer.cpp:777-778, 1378-1551; one lane per vertex, 64 per wave), then the
+// triangle records -> global vertex ids.  Runs after k_vertex wrote the positions.
+template <class EV>
+__device__ __forceinline__ void finish_body(const Params& p, float* lds) {
+    const int wave = threadIdx.x >> 6;
+    const int lane = lane_id();
+    ModelPtr M = as_const(p.model);
+    EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
+    const uint32_t nV = (uint32_t)p.offs[p.mpuCount];
+    const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
+    for (uint32_t b = wave0; b * 64 < nV; b += nWaves) {
+        uint32_t g = b * 64 + lane;
+        const bool valid = g < nV;
+        if (!valid) g = b * 64;
+        const float x = p.pos[g * 3 + 0], y = p.pos[g * 3 + 1], z = p.pos[g * 3 + 2];
+        const CullMask cm = cull_mask_points(M, x, y, z, p.cull != 0);
+        float c[3];
+        (void)ev.template eval<1, true>(x, y, z, cm, c);
+        if (valid) {
+            p.col[g * 3 + 0] = c[0];
+            p.col[g * 3 + 1] = c[1];
+            p.col[g * 3 + 2] = c[2];
+        }
+    }
+    const ShardBatches sb(p.ctr->tShard, p.tShardCap, 64);
+    for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sb.locate(batch, &shard, &first, &count);
+        const uint32_t t = first + lane;
+        if (t >= count) continue;
+        const TriRec R = p.tq[(size_t)shard * p.tShardCap + t];
+        const uint64_t o = p.offs[R.w];
+        const uint32_t gt = (uint32_t)(o >> 32) + R.tlocal;
+        const uint32_t base = (uint32_t)o;
+        p.tris[gt * 3 + 0] = base + (R.v01 & 0xffffu);
+        p.tris[gt * 3 + 1] = base + (R.v01 >> 16);
+        p.tris[gt * 3 + 2] = base + R.v2;
     }
 }
 

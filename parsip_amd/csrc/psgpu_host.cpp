@@ -301,7 +301,7 @@ hipError_t grow(T*& ptr, size_t& cap, size_t need) {
 }
 
 constexpr int kNumKernels = 6;
-const char* kKernelNames[kNumKernels] = {"k_precheck", "select", "k_mpu", "scan", "k_vertex", "k_tris"};
+const char* kKernelNames[kNumKernels] = {"k_precheck", "select", "k_mpu", "scan", "k_vertex", "k_finish"};
 
 }  // namespace
 
@@ -452,7 +452,8 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         if (J) PSGPU_CHECK(launch_jit(J->vertex, persist, 256, 0, s, p));
         else PSGPU_CHECK(launch_vertex(p, s, persist));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
-        PSGPU_CHECK(launch_tris(p, s, persist));
+        if (J) PSGPU_CHECK(launch_jit(J->finish, persist, 256, 0, s, p));
+        else PSGPU_CHECK(launch_finish(p, s, persist));
         if (t) PSGPU_CHECK(hipEventRecord(c->ev[6], s));
     }
     PSGPU_CHECK(hipMemcpyAsync(c->hostCtr, c->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));

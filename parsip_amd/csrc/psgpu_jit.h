@@ -11,7 +11,7 @@ namespace psgpu {
 
 struct JitKernels {
     hipModule_t mod = nullptr;
-    hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, probe = nullptr;
+    hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, finish = nullptr, probe = nullptr;
 };
 
 // Compiled (cached per structure and device) kernels for the model; nullptr + *err on failure.

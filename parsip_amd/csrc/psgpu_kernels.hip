@@ -10,7 +10,7 @@
 //               sums for the reference's discovery order, triangle records
 //   scan        rocPRIM: per-MPU vertex/triangle offsets (compact mesh)
 //   k_vertex    one quad per vertex: S4 4-sample root bracket, S5 colour + normals
-//   k_tris      triangle records -> global vertex ids
+//   k_finish    vertex colours (64 per wave) + triangle records -> global vertex ids
 //
 // The tree-evaluating kernels (precheck, mpu, vertex, probe) exist twice: here with
 // the generic walk-program interpreter (InterpEval), and specialised per model
@@ -44,23 +44,9 @@ __global__ void __launch_bounds__(256) k_probe(Params p, const float* __restrict
     probe_body<InterpEval>(p, plds, xyz, out, colOut, n, mode);
 }
 
-__global__ void __launch_bounds__(256) k_tris(Params p) {
-    const int wave = threadIdx.x >> 6;
-    const ShardBatches sb(p.ctr->tShard, p.tShardCap, 64);
-    const uint32_t nWaves = gridDim.x * 4;
-    for (uint32_t batch = blockIdx.x * 4 + wave; batch < sb.total; batch += nWaves) {
-        uint32_t shard, first, count;
-        sb.locate(batch, &shard, &first, &count);
-        const uint32_t t = first + lane_id();
-        if (t >= count) continue;
-        const TriRec R = p.tq[(size_t)shard * p.tShardCap + t];
-        const uint64_t o = p.offs[R.w];
-        const uint32_t g = (uint32_t)(o >> 32) + R.tlocal;
-        const uint32_t b = (uint32_t)o;
-        p.tris[g * 3 + 0] = b + (R.v01 & 0xffffu);
-        p.tris[g * 3 + 1] = b + (R.v01 >> 16);
-        p.tris[g * 3 + 2] = b + R.v2;
-    }
+__global__ void __launch_bounds__(256) k_finish(Params p) {
+    extern __shared__ __attribute__((aligned(16))) float flds[];
+    finish_body<InterpEval>(p, flds);
 }
 
 // ---------------------------------------------------------------------------
@@ -83,8 +69,8 @@ hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks) {
     hipLaunchKernelGGL(k_vertex, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
-hipError_t launch_tris(const Params& p, hipStream_t s, uint32_t blocks) {
-    hipLaunchKernelGGL(k_tris, dim3(blocks), dim3(256), 0, s, p);
+hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks) {
+    hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
 hipError_t launch_probe(const Params& p, hipStream_t s, const float* xyz, float* out, float* col, uint32_t n,
