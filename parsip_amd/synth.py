@@ -1,7 +1,14 @@
 """Synthetic BlobTrees of the benchmark shapes.
 
-Portable inputs: a splitmix64 stream (seed 42) mapped to fp32 as ``(u >> 40) * 2**-24``
-(never ``std::uniform_real_distribution``, which is implementation defined).
+Centres come from the stream the survey's reference probe used:
+libstdc++ ``std::mt19937(42)`` with ``std::uniform_real_distribution<float>(-2, 2)``,
+drawn x, y, z per primitive.  Both are restated here in pure Python (MT19937 is fixed by
+the C++ standard; libstdc++'s ``generate_canonical<float, 24>`` with a 32-bit engine is
+``float(u) / 2^32`` clamped below 1, then ``r * (b - a) + a`` in fp32), so the inputs are
+identical to the reference run and its recorded outputs pin the oracle:
+C2 1,417 full MPUs / 32,541 V / 50,034 T and C3 19,237 / 339,820 / 520,224.
+The portable splitmix64 stream of §8(d) (``(u >> 40) * 2**-24``) stays available as
+``rng="splitmix64"``.
 
 * C1  1 Point at the origin, no ops, 32^3 cells over [-1,1]^3
 * C2  8 prims (2 per type), 7 ops, 128^3 over [-4,4]^3
@@ -52,6 +59,38 @@ class SplitMix64:
 
     def next_f32(self) -> np.float32:
         return np.float32((self.next_u64() >> 40) * (2.0 ** -24))
+
+
+class MT19937:
+    """std::mt19937 (C++ [rand.predef]: 32-bit Mersenne Twister, default seeding)."""
+
+    def __init__(self, seed: int = 5489):
+        mt = [seed & 0xFFFFFFFF]
+        for i in range(1, 624):
+            mt.append((1812433253 * (mt[-1] ^ (mt[-1] >> 30)) + i) & 0xFFFFFFFF)
+        self.mt = mt
+        self.idx = 624
+
+    def next_u32(self) -> int:
+        if self.idx >= 624:
+            mt = self.mt
+            for i in range(624):
+                y = (mt[i] & 0x80000000) | (mt[(i + 1) % 624] & 0x7FFFFFFF)
+                mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+            self.idx = 0
+        y = self.mt[self.idx]
+        self.idx += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        return y ^ (y >> 18)
+
+    def uniform_f32(self, a: float, b: float) -> np.float32:
+        """libstdc++ uniform_real_distribution<float>(a, b) over this engine."""
+        r = np.float32(self.next_u32()) / np.float32(2.0 ** 32)
+        if r >= 1:
+            r = np.nextafter(np.float32(1), np.float32(0))
+        return np.float32(np.float32(r * np.float32(np.float32(b) - np.float32(a))) + np.float32(a))
 
 
 _F = np.float32
@@ -191,7 +230,7 @@ def build_balanced_ops(model: Model, n_prims: int) -> None:
     O["ctOps"][0] = counter[0]
 
 
-def make_config(name: str, frame: int = 0, seed: int = 42):
+def make_config(name: str, frame: int = 0, seed: int = 42, rng: str = "mt19937"):
     """Return (model, cellsize, N) for one of C1..C5.  ``frame`` animates C5."""
     n_prims, N, half = CONFIGS[name]
     model = Model.empty(name)
@@ -199,9 +238,16 @@ def make_config(name: str, frame: int = 0, seed: int = 42):
         set_prim(model, 0, NodeType.POINT, (0.0, 0.0, 0.0))
         model.prims["ctPrims"][0] = 1
     else:
-        rng = SplitMix64(seed)
+        if rng == "mt19937":
+            gen = MT19937(seed)
+            draw = lambda: gen.uniform_f32(-2.0, 2.0)  # noqa: E731
+        elif rng == "splitmix64":
+            sm = SplitMix64(seed)
+            draw = lambda: _F(-2.0) + _F(4.0) * sm.next_f32()  # noqa: E731
+        else:
+            raise ValueError(f"unknown rng {rng!r}")
         for i in range(n_prims):
-            c = np.array([_F(-2.0) + _F(4.0) * rng.next_f32() for _ in range(3)], np.float32)
+            c = np.array([draw() for _ in range(3)], np.float32)
             if name == "C5":
                 c[0] = np.float32(c[0] + np.float32(0.25 * math.sin(2.0 * math.pi * frame / 60.0 + i)))
             set_prim(model, i, _CYCLE[i % 4], c)

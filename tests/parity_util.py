@@ -37,3 +37,22 @@ def assert_mesh_matches(gmesh, gstats, omesh, normals_atol: float | None = None,
         assert ok.all(), f"normals beyond {normals_atol}: {np.count_nonzero(~ok)}"
     if colours:
         assert_bits_equal(gmesh.col, omesh.col, "vertex colours")
+
+
+def _canon(a: np.ndarray) -> bytes:
+    a = np.ascontiguousarray(a, np.float32).copy()
+    a[np.isnan(a)] = np.float32(np.nan)
+    return a.view(np.uint32).astype("<u4").tobytes()
+
+
+def mesh_digests(stats4, pos, nrm, col, tris_local) -> dict:
+    """SHA-256 digests of a mesh in MPU order; stats4 = (passed, evals, V, T) per MPU."""
+    import hashlib
+
+    h = lambda b: hashlib.sha256(b).hexdigest()  # noqa: E731
+    st = np.ascontiguousarray(stats4, np.uint32)
+    return {"vertices": int(len(pos)), "triangles": int(len(tris_local)),
+            "passed_s1": int(np.count_nonzero(st[:, 0])),
+            "stats_sha256": h(st.astype("<u4").tobytes()),
+            "pos_sha256": h(_canon(pos)), "nrm_sha256": h(_canon(nrm)), "col_sha256": h(_canon(col)),
+            "tris_sha256": h(np.ascontiguousarray(tris_local, np.uint16).astype("<u2").tobytes())}

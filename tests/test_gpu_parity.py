@@ -6,10 +6,13 @@ triangle counts, vertex order and triangle indices bit-exact; positions bit-exac
 1/sqrt (the reference's _mm_rsqrt_ps is CPU-vendor specific: see test_oracle.py for
 the 2e-3 normal tolerance against that variant).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
-from parity_util import assert_bits_equal, assert_mesh_matches
+from parity_util import assert_bits_equal, assert_mesh_matches, mesh_digests
 from parsip_amd import gpu, soa, synth
 from parsip_amd.soa import NodeType
 
@@ -45,6 +48,23 @@ def test_c1_reference_counts(gpu_poly):
     gpu_poly.set_model(model)
     info = gpu_poly.run(cs)
     assert (info.ctMPUs, info.ctPassedPrecheck, info.ctVertices, info.ctTriangles) == (125, 109, 1326, 2024)
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C3"])
+def test_reference_counts_and_golden_digests(gpu_poly, name):
+    """Counts recorded from the reference and the committed oracle digests
+    (tests/golden/oracle_digests.json): full-output parity without running the oracle."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    ref = json.load(open(os.path.join(gdir, "reference_probe.json")))[name]
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
+    model, cs, _ = synth.make_config(name)
+    gpu_poly.set_model(model)
+    info = gpu_poly.run(cs)
+    assert (info.ctMPUs, info.ctPassedPrecheck, info.ctVertices, info.ctTriangles) == \
+        (ref["mpus"], ref["passed_s1"], ref["vertices"], ref["triangles"])
+    gm, gs = gpu_poly.download(), gpu_poly.stats()
+    st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+    assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig
 
 
 def test_c3_full_size(gpu_poly, oracle):

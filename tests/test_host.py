@@ -1,0 +1,126 @@
+"""The C-ABI library on the host (no GPU): it loads, exports every entry point the
+header declares, its host-only helpers agree with the oracle / the reference layout, and
+the run-time specialised kernels compile.  No compute call needs a device here."""
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+from parsip_amd import gpu, soa, synth
+from parsip_amd.soa import NodeType
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        txt = re.sub(r"/\*.*?\*/|//[^\n]*", "", open(h).read(), flags=re.S)
+        names.update(re.findall(r"\b(psgpu_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
+
+
+def test_library_exports_every_header_symbol():
+    L = gpu.load()
+    names = header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(gpu.EXPORTED_SYMBOLS) == set(names)
+
+
+def test_version_string():
+    v = gpu.load().psgpu_version().decode()
+    assert "gfx950" in v
+
+
+def test_soa_layout_matches_reference_sizes():
+    """PS_Polygonizer.h structs, byte-exact (SURVEY.md §8(b) [probe] sizeof/offsetof)."""
+    assert soa.PRIMS_DTYPE.itemsize == 9500
+    assert soa.OPS_DTYPE.itemsize == 5636
+    assert soa.PRIM_MATRICES_DTYPE.itemsize == 6148
+    assert soa.BOX_MATRICES_DTYPE.itemsize == 8196
+    assert soa.MPU_DTYPE.itemsize == 21524
+    f = soa.PRIMS_DTYPE.fields
+    assert f["skeletType"][1] == 9216 and f["idxMatrix"][1] == 9344
+    assert f["bboxLo"][1] == 9472 and f["ctPrims"][1] == 9496
+    o = soa.OPS_DTYPE.fields
+    assert o["vBoxLoX"][1] == 512 and o["resX"][1] == 3584 and o["ctOps"][1] == 5632
+    m = soa.MPU_DTYPE.fields
+    assert (m["vNorm"][1], m["vColor"][1], m["triangles"][1]) == (6144, 12288, 18432)
+    assert (m["ctVertices"][1], m["ctTriangles"][1], m["bboxLo"][1], m["ctFieldEvals"][1]) == \
+        (21504, 21506, 21508, 21520)
+
+
+def test_tritable_equals_oracle(oracle):
+    np.testing.assert_array_equal(gpu.tritable(), oracle.tritable())
+
+
+def test_count_mpus_equals_oracle(oracle):
+    rng = np.random.default_rng(1)
+    for _ in range(100):
+        lo = rng.uniform(-5, 0, 3).astype(np.float32)
+        hi = (lo + rng.uniform(0.1, 9, 3)).astype(np.float32)
+        cs = float(np.float32(rng.uniform(0.01, 0.3)))
+        assert gpu.count_mpus(cs, lo, hi) == oracle.count_mpus(cs, lo, hi)
+
+
+def test_prepare_bboxes_equals_oracle(oracle):
+    types = [NodeType.POINT, NodeType.LINE, NodeType.CYLINDER, NodeType.CUBE, NodeType.DISC,
+             NodeType.RING, NodeType.TRIANGLE]
+    for seed in range(6):
+        m = synth.random_model(seed, 4 + 3 * seed, types=types, matrices=seed % 2 == 1)
+        a, b = m.copy(), m.copy()
+        assert oracle.prepare_bboxes(a) == 1
+        assert gpu.prepare_bboxes(0.05, b) == 1
+        assert a.prims.tobytes() == b.prims.tobytes()
+        assert a.ops.tobytes() == b.ops.tobytes()
+
+
+def test_translate_blobtree_type():
+    """_constSettings.h codes -> PS_Polygonizer.h codes (SURVEY.md §8(b) Enum row)."""
+    L = gpu.load()
+    expect = {0: NodeType.POINT, 1: NodeType.LINE, 2: NodeType.CYLINDER, 3: NodeType.DISC, 4: NodeType.RING,
+              14: NodeType.UNION, 15: NodeType.INTERSECT, 16: NodeType.DIF, 17: NodeType.SMOOTHDIF,
+              18: NodeType.BLEND, 19: NodeType.RICCIBLEND, 20: NodeType.GRADIENTBLEND, 24: NodeType.WARPTWIST,
+              13: -1, -1: -1, 99: -1}
+    for code, want in expect.items():
+        assert L.psgpu_translate_blobtree_type(code) == want == soa.translate_blobtree_type(code), code
+    for code in range(-2, 40):
+        assert L.psgpu_translate_blobtree_type(code) == soa.translate_blobtree_type(code)
+
+
+def test_mpu_dims_and_limits():
+    L = gpu.load()
+    m, cs, n = synth.make_config("C3")
+    dims = np.zeros(3, np.uint32)
+    assert L.psgpu_mpu_dims(cs, m.prims.ctypes.data, dims.ctypes.data) == 1
+    assert tuple(dims) == soa.mpu_dims(cs, *m.bbox) == (37, 37, 37)
+
+
+def test_no_device_fails_loudly():
+    """Without a visible GPU the product path raises; there is no CPU fallback."""
+    if gpu.device_count() > 0:
+        pytest.skip("a device is visible")
+    with pytest.raises(gpu.PsgpuError):
+        gpu.Polygonizer(0)
+
+
+def test_invalid_trees_rejected():
+    """The walk-program builder rejects what the reference adapter rejects (-3)."""
+    m, cs, _ = synth.make_config("C2")
+    bad = m.copy()
+    bad.ops["opLeftChild"][0, 1] = 0  # cycle back to the root
+    bad.ops["opChildKind"][0, 1] |= 2
+    with pytest.raises(gpu.PsgpuError) as e:
+        gpu.jit_compile(bad, 1)
+    assert e.value.code == soa.RET_INVALID_BVH
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_jit_compiles_c3(mode):
+    """hiprtc specialisation of the C3 tree compiles for gfx950 without a device."""
+    m, _, _ = synth.make_config("C3")
+    assert gpu.jit_compile(m, mode) > 10000
