@@ -161,7 +161,7 @@ def main():
     evals = costmodel.lane_evals(info.ctMPUs, info.ctPassedPrecheck, info.ctVertices)
     per_eval = costmodel.ops_per_eval(model)
     kernel_evals = {"k_precheck": 8 * info.ctMPUs, "k_mpu": 512 * info.ctPassedPrecheck,
-                    "k_vertex": 8 * info.ctVertices, "k_finish": info.ctVertices}
+                    "k_vertex": 7 * info.ctVertices, "k_finish": info.ctVertices}
     dom_flops = kernel_evals.get(dom, evals) * per_eval
     achieved = dom_flops / (kt[dom] * 1e-3) / 1e12
     counts = grp.allgather([info.ctVertices, info.ctTriangles])
@@ -178,7 +178,7 @@ def main():
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (splitmix64 seed 42 BlobTree, SURVEY.md §8(d))",
+        "data": "synthetic: C3 BlobTree from std::mt19937(42) as in the reference probe (SURVEY.md §6, §8(d))",
         "config": {"workload": f"{args.config}: {model.ct_prims}-prim/{model.ct_ops}-op BlobTree, {N}^3 cells, "
                                f"{n_mpus} MPUs" + (f", frame=rank" if args.scaling == "weak" and grp.world > 1 else ""),
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,

@@ -148,15 +148,16 @@ typedef struct PsMeshInfo {
 
 /* Device-resident compact mesh of the last polygonization (pointers into the
  * context's HBM buffers; valid until the next psgpu_polygonize on the context).
- * Vertices of slot w occupy [(uint32)mpuOffsets[w], (uint32)mpuOffsets[w+1]) in MPU order,
- * i.e. exactly the reference's concatenation of vMPUs[i].vPos over i.              */
+ * The vertices of the w-th MPU of the processed range [mpuBegin, mpuEnd) occupy
+ * [(uint32)mpuOffsets[w], (uint32)mpuOffsets[w+1]) and its triangles
+ * [mpuOffsets[w] >> 32, mpuOffsets[w+1] >> 32): MPU order, i.e. exactly the reference's
+ * concatenation of vMPUs[i].vPos / triangles over i (PS_Polygonizer.cpp:360-371).   */
 typedef struct PsMeshDevice {
     const float*    pos;              /* ctVertices * 3, xyz interleaved           */
     const float*    nrm;              /* ctVertices * 3                            */
     const float*    col;              /* ctVertices * 3                            */
     const uint32_t* tris;             /* ctTriangles * 3, global vertex ids        */
-    const uint32_t* surfaceMpuIds;    /* ctPassedPrecheck: global MPU id per slot  */
-    const uint64_t* mpuOffsets;       /* ctPassedPrecheck + 1, exclusive scan:
+    const uint64_t* mpuOffsets;       /* ctMPUs + 1, exclusive scan:
                                          vertexOffset | triangleOffset << 32      */
 } PsMeshDevice;
 
@@ -193,10 +194,10 @@ int  psgpu_polygonize(psgpu_ctx* ctx, float cellsize, uint32_t mpuBegin, uint32_
  * buffers were too small the call re-runs the polygonization with grown buffers. */
 int  psgpu_finish(psgpu_ctx* ctx, PsMeshInfo* info);
 int  psgpu_mesh_device(psgpu_ctx* ctx, PsMeshDevice* out);
-/* Copy the compact mesh to host arrays (any pointer may be NULL). */
+/* Copy the compact mesh to host arrays (any pointer may be NULL); mpuOffsets gets
+ * ctMPUs + 1 entries as in PsMeshDevice. */
 int  psgpu_download_mesh(psgpu_ctx* ctx, float* pos, float* nrm, float* col, uint32_t* tris,
-                         uint32_t* surfaceMpuIds, uint32_t* mpuVertexOffset,
-                         uint32_t* mpuTriangleOffset);
+                         uint64_t* mpuOffsets);
 /* Per-MPU stats for every MPU in the last processed range (ctMPUs entries). */
 int  psgpu_download_stats(psgpu_ctx* ctx, PsMpuStats* stats);
 /* Scatter the last result into the reference PolyMPUs layout (vMPUs[0..ctMPUs)). */

@@ -57,24 +57,49 @@ __device__ __forceinline__ bool group_any(bool v) {
     return v;
 }
 
+// Cross-lane work on DPP (no LDS crossbar round trips): quad_perm [1,0,3,2] = 0xB1,
+// [2,3,0,1] = 0x4E, row_half_mirror = 0x141, row_mirror = 0x140, row_shr:n = 0x110 + n,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143.
+#define PSGPU_DPP_F(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xF, 0xF, false))
+
+// Value of lane S of this lane's quad.
+template <int S>
+__device__ __forceinline__ float quad_bcast(float v) { return PSGPU_DPP_F(v, S * 0x55); }
+
+// Wave-uniform min / max (NaNs must be excluded by the caller).
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
-    return v;
+    v = fminf(v, PSGPU_DPP_F(v, 0xB1));
+    v = fminf(v, PSGPU_DPP_F(v, 0x4E));
+    v = fminf(v, PSGPU_DPP_F(v, 0x141));
+    v = fminf(v, PSGPU_DPP_F(v, 0x140));
+    return fminf(fminf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))),
+                 fminf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    v = fmaxf(v, PSGPU_DPP_F(v, 0xB1));
+    v = fmaxf(v, PSGPU_DPP_F(v, 0x4E));
+    v = fmaxf(v, PSGPU_DPP_F(v, 0x141));
+    v = fmaxf(v, PSGPU_DPP_F(v, 0x140));
+    return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))),
+                 fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
+}
+// Inclusive prefix sum over the wave (Hillis-Steele in 16-lane rows, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
     return v;
 }
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o);
-        if (l >= o) v += t;
-    }
-    return v;
+// Value of a wave-uniform lane (scalar read).
+__device__ __forceinline__ uint32_t lane_value(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -453,13 +478,20 @@ __device__ __forceinline__ void mpu_origin(const Params& p, uint32_t m, float o[
     o[2] = p.lo[2] + (float)k * p.side;
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wave_incl_scan(v), 63); }
+
 // S1: 8 corners per MPU, lanes 0-3 z = lo, lanes 4-7 z = lo + side; (x,y) lanes
 // (0,0),(1,0),(0,1),(1,1) (PS_Polygonizer.cpp:488-519).  256 threads = 32 MPUs.
+// Failing MPUs get count 0 here; survivors are appended to the sharded queue pq (one
+// atomic per wave; waves [s*K, (s+1)*K) with K = ceil(waves / 64) append to shard s,
+// so a shard holds at most 8K = pShardCap ids).  k_mpu takes them in any order: the mesh
+// order comes from k_scan over the per-MPU counts.
 template <class EV>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
-    EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane_id());
-    const uint32_t local = (blockIdx.x * 256 + threadIdx.x) >> 3;
+    const int lane = lane_id();
+    EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
+    const uint32_t local = blockIdx.x * 32u + (threadIdx.x >> 3);
     const bool valid = local < p.mpuCount;
     const uint32_t m = p.mpuBegin + (valid ? local : 0);
     float o[3];
@@ -471,13 +503,21 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const float pz = Z * p.side + o[2];
     const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
     const float f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
-    const uint64_t b = ballot(valid && f > 0.0f);
-    if (lane_id() == 0) {  // one flag byte per MPU: 8 MPUs per wave, one 8-byte store
-        uint64_t flags = 0;
+    const uint64_t bal = ballot(valid && f > 0.0f);
+    uint32_t flags8 = 0;  // bit g: MPU of lanes 8g..8g+7 passed
 #pragma unroll
-        for (int g = 0; g < 8; ++g) flags |= (((b >> (8 * g)) & 0xffull) != 0ull ? 1ull : 0ull) << (8 * g);
-        reinterpret_cast<uint64_t*>(p.passFlags)[blockIdx.x * 4 + wave] = flags;
-    }
+    for (int g = 0; g < 8; ++g) flags8 |= (((bal >> (8 * g)) & 0xffull) != 0ull ? 1u : 0u) << g;
+    const uint32_t mine = blockIdx.x * 32u + (uint32_t)wave * 8u + (uint32_t)lane;  // lanes 0..7: MPU g = lane
+    const bool pass = lane < 8 && ((flags8 >> lane) & 1u);
+    if (lane < 8 && !pass && mine < p.mpuCount) p.counts[mine] = 0ull;
+    if (flags8 == 0u) return;
+    // shard = slab of consecutive precheck waves: k_mpu then walks the survivors roughly
+    // in MPU order (neighbouring waves share culling masks and model cache lines)
+    const uint32_t shard = (blockIdx.x * 4u + (uint32_t)wave) / (p.pShardCap / 8u);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(flags8));
+    base = lane_value(base, 0);
+    if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(flags8 & ((1u << lane) - 1u))] = p.mpuBegin + mine;
 }
 
 #ifndef PSGPU_S2_N
@@ -499,6 +539,12 @@ template <class EV>
 __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
+    // block b, wave v: entry (b % B) * 4 + v of survivor shard b / B, B = pShardCap / 4
+    const uint32_t bps = p.pShardCap / 4u;
+    const uint32_t pshard = blockIdx.x / bps;
+    const uint32_t pidx = (blockIdx.x % bps) * 4u + (uint32_t)wave;
+    const uint32_t pcount = p.ctr->shard[pshard].p;
+    if ((blockIdx.x % bps) * 4u >= pcount) return;  // whole block past the shard's end
     // stage the tables in LDS (every wave of the block takes part before any exits)
     CubeTablesDev* tab = reinterpret_cast<CubeTablesDev*>(smem);
     {
@@ -507,9 +553,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         for (int i = threadIdx.x; i < (int)(sizeof(CubeTablesDev) / 4); i += blockDim.x) dst[i] = src[i];
     }
     __syncthreads();
-    const uint32_t w = blockIdx.x * 4 + wave;
-    const uint32_t passCount = p.ctr->passCount;
-    if (w >= passCount) return;
+    if (pidx >= pcount) return;
     unsigned char* base = smem + kLdsTables + wave * (kLdsSlots + p.slotsPerLane * 64 * 4);
     float* fv = reinterpret_cast<float*>(base + kLdsFv);
     uint16_t* edgeVid = reinterpret_cast<uint16_t*>(base + kLdsEdge);
@@ -519,7 +563,8 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     ModelPtr M = as_const(p.model);
     EV ev(M, reinterpret_cast<float*>(base + kLdsSlots) + lane);
 
-    const uint32_t m = __builtin_amdgcn_readfirstlane(p.passList[w]);
+    const uint32_t m = __builtin_amdgcn_readfirstlane(p.pq[pshard * p.pShardCap + pidx]);
+    const uint32_t w = m - p.mpuBegin;  // slot of the MPU in the range: counts / offsets index
     float o[3];
     mpu_origin(p, m, o);
     const float cs = p.cs;
@@ -556,7 +601,10 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         fv[x * 64 + lane] = fs8[x];
         inside += __popcll(ballot(fs8[x] >= 0.5f));
     }
-    if (inside == 0 || inside == 512 || (p.debug & 1u)) return;  // counts stay zero
+    if (inside == 0 || inside == 512 || (p.debug & 1u)) {  // no vertices, no triangles
+        if (lane == 0) p.counts[w] = 0ull;
+        return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
@@ -589,21 +637,21 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
             cellV[c] = (uint16_t)(carryV + sv - nv);
             cellT[c] = (uint16_t)(carryT + st - nt);
         }
-        carryV += __shfl(sv, 63);
-        carryT += __shfl(st, 63);
+        carryV += lane_value(sv, 63);
+        carryT += lane_value(st, 63);
     }
     const uint32_t V = carryV, T = carryT;
-    const uint32_t shard = w & (kShards - 1);
+    const uint32_t shard = (blockIdx.x * 4u + (uint32_t)wave) & (kShards - 1);
     uint32_t qv = 0, qt = 0;
     if (lane == 0) {
-        qv = atomicAdd(&p.ctr->vShard[shard], V);
-        qt = atomicAdd(&p.ctr->tShard[shard], T);
+        qv = atomicAdd(&p.ctr->shard[shard].v, V);
+        qt = atomicAdd(&p.ctr->shard[shard].t, T);
         p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
-        if (T > 0) atomicAdd(&p.ctr->sShard[shard], 1u);
+        if (T > 0) atomicAdd(&p.ctr->shard[shard].s, 1u);
         if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
     }
-    qv = __shfl(qv, 0);
-    qt = __shfl(qt, 0);
+    qv = lane_value(qv, 0);
+    qt = lane_value(qt, 0);
     VertexRec* vq = p.vq + (size_t)shard * p.vShardCap;
     TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -669,10 +717,10 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
 struct ShardBatches {
     uint32_t cnt, incl, total;
     __device__ ShardBatches(const uint32_t* counts, uint32_t cap, uint32_t per) {
-        cnt = min(counts[lane_id()], cap);
+        cnt = min(counts[lane_id() * (sizeof(ShardCtr) / 4)], cap);  // one counter per shard line
         const uint32_t nb = (cnt + per - 1) / per;
         incl = wave_incl_scan(nb);
-        total = __shfl(incl, kShards - 1);
+        total = lane_value(incl, kShards - 1);
         perBatch = per;
         nbat = nb;
     }
@@ -701,7 +749,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const float r = (float)j * third;
     const float delta = 0.001f;
     const float inv = -1.0f / delta;
-    const ShardBatches sb(p.ctr->vShard, p.vShardCap, 16);
+    const ShardBatches sb(&p.ctr->shard[0].v, p.vShardCap, 16);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
@@ -724,14 +772,17 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         e2[ax] = e1[ax] + cs;
         const float dX = e2[0] - e1[0], dY = e2[1] - e1[1], dZ = e2[2] - e1[2];
         const float qx = e1[0] + dX * r, qy = e1[1] + dY * r, qz = e1[2] + dZ * r;
-        // one cull box for both phases: the edge samples' AABB grown by delta covers p + delta*e_a
+        // the edge samples' AABB grown by delta also covers p + delta*e_a whenever p lies on
+        // the bracketing segment (0 <= scale <= 1); phase B recomputes the mask otherwise
         const CullMask cm = cull_mask_points(M, qx, qy, qz, p.cull != 0, delta);
         const float f = ev.template eval<4, false>(qx, qy, qz, cm, nullptr);
-        const int qb = lane & ~3;
         float fs[4], xs[4], ys[4], zs[4];
+        fs[0] = quad_bcast<0>(f);
+        fs[1] = quad_bcast<1>(f);
+        fs[2] = quad_bcast<2>(f);
+        fs[3] = quad_bcast<3>(f);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            fs[s] = __shfl(f, qb + s);
             const float rs = (float)s * third;
             xs[s] = e1[0] + dX * rs;
             ys[s] = e1[1] + dY * rs;
@@ -757,9 +808,12 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         const float qz2 = j == 3 ? P2 + delta : P2;
         // fieldValue at p and at the three normal samples; the colour walk at p runs in
         // finish_body, 64 vertices per wave (colour work is needed at 1 point in 4)
-        const float g = ev.template eval<1, false>(qx2, qy2, qz2, cm, nullptr);
-        const float vtx = __shfl(g, qb);
-        const float gx = __shfl(g, qb + 1), gy = __shfl(g, qb + 2), gz = __shfl(g, qb + 3);
+        // p off its edge (no sign change in the samples, or inf/NaN): box of the actual points
+        const bool onEdge = scale >= 0.0f && scale <= 1.0f;
+        const CullMask cmB = ballot(!onEdge) == 0ull ? cm : cull_mask_points(M, qx2, qy2, qz2, p.cull != 0);
+        const float g = ev.template eval<1, false>(qx2, qy2, qz2, cmB, nullptr);
+        const float vtx = quad_bcast<0>(g);
+        const float gx = quad_bcast<1>(g), gy = quad_bcast<2>(g), gz = quad_bcast<3>(g);
         float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
         const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);  // SimdNormalize
         nx = nx * im;
@@ -785,6 +839,16 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const uint32_t nV = (uint32_t)p.offs[p.mpuCount];
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (blockIdx.x == 0) {  // the run's counters for the host (mapped pinned memory)
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.ctr);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(p.hostCtr);
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) dst[i] = src[i];
+        __threadfence_system();
+        // the next run's counters and k_scan words (no kernel of this run touches them)
+        uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
+        for (uint32_t i = threadIdx.x; i < kScanMaxBlocks; i += blockDim.x) p.scanStatusNext[i] = 0ull;
+    }
     for (uint32_t b = wave0; b * 64 < nV; b += nWaves) {
         uint32_t g = b * 64 + lane;
         const bool valid = g < nV;
@@ -799,7 +863,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
             p.col[g * 3 + 2] = c[2];
         }
     }
-    const ShardBatches sb(p.ctr->tShard, p.tShardCap, 64);
+    const ShardBatches sb(&p.ctr->shard[0].t, p.tShardCap, 64);
     for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
         sb.locate(batch, &shard, &first, &count);

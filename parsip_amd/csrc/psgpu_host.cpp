@@ -300,8 +300,8 @@ hipError_t grow(T*& ptr, size_t& cap, size_t need) {
     return e;
 }
 
-constexpr int kNumKernels = 6;
-const char* kKernelNames[kNumKernels] = {"k_precheck", "select", "k_mpu", "scan", "k_vertex", "k_finish"};
+constexpr int kNumKernels = 5;
+const char* kKernelNames[kNumKernels] = {"k_precheck", "k_mpu", "k_scan", "k_vertex", "k_finish"};
 
 }  // namespace
 
@@ -328,23 +328,22 @@ struct psgpu_ctx {
     bool pending = false;
     bool haveResult = false;
     // device buffers
-    size_t capFlags = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
-    size_t capTemp = 0;
-    uint8_t* passFlags = nullptr;
-    uint32_t* passList = nullptr;
+    size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
+    uint32_t* pq = nullptr;         // sharded S1 survivor queues
+    uint32_t pShardCap = 0;
+    uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
+    uint32_t parity = 0;            // which counter / status set the next run uses
     uint64_t* counts = nullptr;
     uint64_t* offs = nullptr;
-    unsigned char* temp = nullptr;  // rocPRIM scratch
     VertexRec* vq = nullptr;
     TriRec* tq = nullptr;
     float* pos = nullptr;
     float* nrm = nullptr;
     float* col = nullptr;
     uint32_t* tris = nullptr;
-    DevCounters* ctr = nullptr;
-    uint32_t* dequeue = nullptr;
-    DevCounters* hostCtr = nullptr;  // pinned
-    DevCounters* initCtr = nullptr;  // pinned template
+    DevCounters* ctr = nullptr;         // two sets, alternating runs
+    DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
+    DevCounters* hostCtrDev = nullptr;  // its device address
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
     uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
     hipEvent_t ev[kNumKernels + 1] = {};
@@ -368,14 +367,10 @@ int hip_fail(hipError_t e, const char* what) {
 
 int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     const size_t n = std::max<uint32_t>(mpuCount, 1);
-    PSGPU_CHECK(grow(c->passFlags, c->capFlags, (n + 31) / 32 * 32));
-    PSGPU_CHECK(grow(c->passList, c->capList, n));
+    c->pShardCap = 8u * (uint32_t)(((n + 7) / 8 + kShards - 1) / kShards);
+    PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
     PSGPU_CHECK(grow(c->offs, c->capOff, n + 1));
-    size_t b1 = 0, b2 = 0;
-    PSGPU_CHECK(select_passing(nullptr, b1, c->passFlags, 0, c->passList, &c->ctr->passCount, (uint32_t)n, c->stream));
-    PSGPU_CHECK(scan_counts(nullptr, b2, c->counts, c->offs, (uint32_t)n, c->stream));
-    PSGPU_CHECK(grow(c->temp, c->capTemp, std::max(b1, b2) + 256));
     PSGPU_CHECK(grow(c->vq, c->capVq, (size_t)c->vShardCap * kShards));
     PSGPU_CHECK(grow(c->tq, c->capTq, (size_t)c->tShardCap * kShards));
     size_t capV2 = c->capV, capV3 = c->capV;
@@ -399,8 +394,14 @@ Params make_params(psgpu_ctx* c) {
     p.mpuBegin = c->mpuBegin;
     p.mpuCount = c->mpuCount;
     p.cull = (uint32_t)c->cull;
-    p.passFlags = c->passFlags;
-    p.passList = c->passList;
+    p.preBlocks = (c->mpuCount + 31) / 32;
+    p.pq = c->pq;
+    p.pShardCap = c->pShardCap;
+    p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
+    if (p.scanChunks == 0) p.scanChunks = 1;
+    p.scanBlocks = (c->mpuCount + kScanItems * p.scanChunks - 1) / (kScanItems * p.scanChunks);
+    p.scanStatus = c->scanStatus + (size_t)c->parity * kScanMaxBlocks;
+    p.scanStatusNext = c->scanStatus + (size_t)(c->parity ^ 1u) * kScanMaxBlocks;
     p.counts = c->counts;
     p.offs = c->offs;
     p.vq = c->vq;
@@ -411,8 +412,9 @@ Params make_params(psgpu_ctx* c) {
     p.nrm = c->nrm;
     p.col = c->col;
     p.tris = c->tris;
-    p.ctr = c->ctr;
-    p.dequeue = c->dequeue;
+    p.ctr = c->ctr + c->parity;
+    p.ctrNext = c->ctr + (c->parity ^ 1u);
+    p.hostCtr = c->hostCtrDev;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     p.debug = (uint32_t)c->debug;
     return p;
@@ -423,40 +425,44 @@ hipError_t launch_jit(hipFunction_t f, uint32_t blocks, uint32_t threads, size_t
     return hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, (unsigned)lds, s, args, nullptr);
 }
 
+// One polygonization = 5 kernels, no copies or fills: k_precheck resets the counters,
+// k_finish publishes them to mapped host memory.
 int enqueue(psgpu_ctx* c, hipStream_t s) {
-    Params p = make_params(c);
-    PSGPU_CHECK(hipMemcpyAsync(c->ctr, c->initCtr, sizeof(DevCounters), hipMemcpyHostToDevice, s));
-    PSGPU_CHECK(hipMemsetAsync(c->dequeue, 0, 4 * sizeof(uint32_t), s));
-    if (c->mpuCount > 0) {
-        PSGPU_CHECK(hipMemsetAsync(c->counts, 0, (size_t)c->mpuCount * sizeof(uint64_t), s));
-        PSGPU_CHECK(hipMemsetAsync(c->offs, 0, sizeof(uint64_t), s));
+    if (c->mpuCount == 0) {
+        memset(c->hostCtr, 0, sizeof(DevCounters));
+    c->hostCtr->firstOverflow = 0x7fffffff;
+    {
+        DevCounters init[2];
+        memset(init, 0, sizeof(init));
+        init[0].firstOverflow = init[1].firstOverflow = 0x7fffffff;
+        if (hipMemcpy(c->ctr, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) {
+            psgpu_destroy(c);
+            return PSGPU_RET_DEVICE_ERROR;
+        }
     }
+        c->hostCtr->firstOverflow = 0x7fffffff;
+        return PSGPU_RET_SUCCESS;
+    }
+    Params p = make_params(c);
+    c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool t = c->timing != 0;
     const uint32_t persist = (uint32_t)c->numCUs * 4;
     JitKernels* J = c->jit.get();
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
-    if (c->mpuCount > 0) {
-        if (J) PSGPU_CHECK(launch_jit(J->precheck, (p.mpuCount + 31) / 32, 256, 0, s, p));
-        else PSGPU_CHECK(launch_precheck(p, s));
-        if (t) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-        size_t tb = c->capTemp;
-        PSGPU_CHECK(select_passing(c->temp, tb, c->passFlags, c->mpuBegin, c->passList, &c->ctr->passCount,
-                                   c->mpuCount, s));
-        if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
-        if (J) PSGPU_CHECK(launch_jit(J->mpu, (p.mpuCount + 3) / 4, 256, mpu_lds_bytes(0), s, p));
-        else PSGPU_CHECK(launch_mpu(p, s));
-        if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-        tb = c->capTemp;
-        PSGPU_CHECK(scan_counts(c->temp, tb, c->counts, c->offs, c->mpuCount, s));
-        if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
-        if (J) PSGPU_CHECK(launch_jit(J->vertex, persist, 256, 0, s, p));
-        else PSGPU_CHECK(launch_vertex(p, s, persist));
-        if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
-        if (J) PSGPU_CHECK(launch_jit(J->finish, persist, 256, 0, s, p));
-        else PSGPU_CHECK(launch_finish(p, s, persist));
-        if (t) PSGPU_CHECK(hipEventRecord(c->ev[6], s));
-    }
-    PSGPU_CHECK(hipMemcpyAsync(c->hostCtr, c->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+    if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
+    else PSGPU_CHECK(launch_precheck(p, s));
+    if (t) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
+    if (J) PSGPU_CHECK(launch_jit(J->mpu, kShards * ((p.pShardCap + 3) / 4), 256, mpu_lds_bytes(0), s, p));
+    else PSGPU_CHECK(launch_mpu(p, s));
+    if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
+    PSGPU_CHECK(launch_scan(p, s));
+    if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
+    if (J) PSGPU_CHECK(launch_jit(J->vertex, persist, 256, 0, s, p));
+    else PSGPU_CHECK(launch_vertex(p, s, persist));
+    if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
+    if (J) PSGPU_CHECK(launch_jit(J->finish, persist, 256, 0, s, p));
+    else PSGPU_CHECK(launch_finish(p, s, persist));
+    if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
     return PSGPU_RET_SUCCESS;
 }
 
@@ -637,15 +643,25 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
         hipMalloc(&c->dTables, sizeof(CubeTablesDev)) != hipSuccess ||
         hipMemcpy(c->dTables, &tabHost, sizeof(CubeTablesDev), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&c->dModel, sizeof(DevModel)) != hipSuccess ||
-        hipMalloc(&c->ctr, sizeof(DevCounters)) != hipSuccess ||
-        hipMalloc(&c->dequeue, 4 * sizeof(uint32_t)) != hipSuccess ||
-        hipHostMalloc(&c->hostCtr, sizeof(DevCounters), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&c->initCtr, sizeof(DevCounters), hipHostMallocDefault) != hipSuccess) {
+        hipMalloc(&c->ctr, 2 * sizeof(DevCounters)) != hipSuccess ||
+        hipMalloc(&c->scanStatus, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(c->scanStatus, 0, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc(&c->hostCtr, sizeof(DevCounters), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hostCtrDev), c->hostCtr, 0) != hipSuccess) {
         psgpu_destroy(c);
         return PSGPU_RET_DEVICE_ERROR;
     }
-    memset(c->initCtr, 0, sizeof(DevCounters));
-    c->initCtr->firstOverflow = 0x7fffffff;
+    memset(c->hostCtr, 0, sizeof(DevCounters));
+    c->hostCtr->firstOverflow = 0x7fffffff;
+    {
+        DevCounters init[2];
+        memset(init, 0, sizeof(init));
+        init[0].firstOverflow = init[1].firstOverflow = 0x7fffffff;
+        if (hipMemcpy(c->ctr, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) {
+            psgpu_destroy(c);
+            return PSGPU_RET_DEVICE_ERROR;
+        }
+    }
     for (int i = 0; i <= kNumKernels; ++i) (void)hipEventCreate(&c->ev[i]);
     const char* cullEnv = getenv("PSGPU_CULL");
     if (cullEnv) c->cull = atoi(cullEnv) != 0;
@@ -660,12 +676,11 @@ void psgpu_destroy(psgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->jit.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->passFlags, c->passList, c->counts, c->offs, c->temp, c->vq, c->tq,
-                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->dequeue};
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->offs, c->vq, c->tq,
+                    c->pos, c->nrm, c->col, c->tris, c->ctr};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hostCtr) (void)hipHostFree(c->hostCtr);
-    if (c->initCtr) (void)hipHostFree(c->initCtr);
     for (int i = 0; i <= kNumKernels; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -749,10 +764,10 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             const DevCounters& h = *c->hostCtr;
             uint32_t V = 0, T = 0, mv = 0, mt = 0;
             for (int k = 0; k < kShards; ++k) {
-                V += h.vShard[k];
-                T += h.tShard[k];
-                mv = std::max(mv, h.vShard[k]);
-                mt = std::max(mt, h.tShard[k]);
+                V += h.shard[k].v;
+                T += h.shard[k].t;
+                mv = std::max(mv, h.shard[k].v);
+                mt = std::max(mt, h.shard[k].t);
             }
             if (V <= c->vcap && T <= c->tcap && mv <= c->vShardCap && mt <= c->tShardCap) break;
             c->vcap = std::max(c->vcap, V + V / 8 + 1024);
@@ -772,16 +787,21 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             }
         }
         const DevCounters& h = *c->hostCtr;
-        uint32_t V = 0, T = 0, S = 0;
+        if (c->mpuCount && h.error) {
+            fprintf(stderr, "psgpu: device protocol error 0x%x\n", h.error);
+            return PSGPU_RET_DEVICE_ERROR;
+        }
+        uint32_t V = 0, T = 0, S = 0, P = 0;
         for (int k = 0; k < kShards; ++k) {
-            V += h.vShard[k];
-            T += h.tShard[k];
-            S += h.sShard[k];
+            V += h.shard[k].v;
+            T += h.shard[k].t;
+            S += h.shard[k].s;
+            P += h.shard[k].p;
         }
         PsMeshInfo& I = c->info;
         memset(&I, 0, sizeof(I));
         I.ctMPUs = c->mpuCount;
-        I.ctPassedPrecheck = c->mpuCount ? h.passCount : 0;
+        I.ctPassedPrecheck = c->mpuCount ? P : 0;
         I.ctSurfaceMPUs = c->mpuCount ? S : 0;
         I.ctVertices = c->mpuCount ? V : 0;
         I.ctTriangles = c->mpuCount ? T : 0;
@@ -812,55 +832,63 @@ int psgpu_mesh_device(psgpu_ctx* c, PsMeshDevice* out) {
     out->nrm = c->nrm;
     out->col = c->col;
     out->tris = c->tris;
-    out->surfaceMpuIds = c->passList;
     out->mpuOffsets = c->offs;
     return PSGPU_RET_SUCCESS;
 }
 
-int psgpu_download_mesh(psgpu_ctx* c, float* pos, float* nrm, float* col, uint32_t* tris, uint32_t* ids,
-                        uint32_t* voff, uint32_t* toff) {
+int psgpu_download_mesh(psgpu_ctx* c, float* pos, float* nrm, float* col, uint32_t* tris, uint64_t* mpuOffsets) {
     PsMeshInfo I;
     int rc = psgpu_finish(c, &I);
     if (rc != PSGPU_RET_SUCCESS) return rc;
-    const size_t V = I.ctVertices, T = I.ctTriangles, W = I.ctPassedPrecheck;
+    const size_t V = I.ctVertices, T = I.ctTriangles, N = I.ctMPUs;
     if (pos && V) PSGPU_CHECK(hipMemcpy(pos, c->pos, V * 12, hipMemcpyDeviceToHost));
     if (nrm && V) PSGPU_CHECK(hipMemcpy(nrm, c->nrm, V * 12, hipMemcpyDeviceToHost));
     if (col && V) PSGPU_CHECK(hipMemcpy(col, c->col, V * 12, hipMemcpyDeviceToHost));
     if (tris && T) PSGPU_CHECK(hipMemcpy(tris, c->tris, T * 12, hipMemcpyDeviceToHost));
-    if (ids && W) PSGPU_CHECK(hipMemcpy(ids, c->passList, W * 4, hipMemcpyDeviceToHost));
-    if (voff || toff) {
-        std::vector<uint64_t> o(W + 1, 0);
-        if (W) PSGPU_CHECK(hipMemcpy(o.data(), c->offs, (W + 1) * 8, hipMemcpyDeviceToHost));
-        for (size_t w = 0; w <= W; ++w) {
-            if (voff) voff[w] = (uint32_t)o[w];
-            if (toff) toff[w] = (uint32_t)(o[w] >> 32);
-        }
+    if (mpuOffsets) {
+        if (N) PSGPU_CHECK(hipMemcpy(mpuOffsets, c->offs, (N + 1) * 8, hipMemcpyDeviceToHost));
+        else mpuOffsets[0] = 0;
     }
     return PSGPU_RET_SUCCESS;
 }
+
+namespace {
+// S1 survivors of the last run (global ids, ascending), gathered from the shard queues.
+int survivors(psgpu_ctx* c, std::vector<uint32_t>& ids) {
+    ids.clear();
+    if (!c->mpuCount) return PSGPU_RET_SUCCESS;
+    const DevCounters& h = *c->hostCtr;
+    std::vector<uint32_t> all((size_t)c->pShardCap * kShards);
+    PSGPU_CHECK(hipMemcpy(all.data(), c->pq, all.size() * 4, hipMemcpyDeviceToHost));
+    for (int k = 0; k < kShards; ++k)
+        ids.insert(ids.end(), all.begin() + (size_t)k * c->pShardCap,
+                   all.begin() + (size_t)k * c->pShardCap + std::min(h.shard[k].p, c->pShardCap));
+    std::sort(ids.begin(), ids.end());
+    return PSGPU_RET_SUCCESS;
+}
+}  // namespace
 
 int psgpu_download_stats(psgpu_ctx* c, PsMpuStats* stats) {
     PsMeshInfo I;
     int rc = psgpu_finish(c, &I);
     if (rc != PSGPU_RET_SUCCESS || !stats) return rc == PSGPU_RET_SUCCESS ? PSGPU_RET_PARAM_ERROR : rc;
-    const uint32_t W = I.ctPassedPrecheck;
-    std::vector<uint32_t> ids(W);
-    std::vector<uint64_t> cnt(W);
-    if (W) {
-        PSGPU_CHECK(hipMemcpy(ids.data(), c->passList, W * 4, hipMemcpyDeviceToHost));
-        PSGPU_CHECK(hipMemcpy(cnt.data(), c->counts, (size_t)W * 8, hipMemcpyDeviceToHost));
-    }
+    std::vector<uint32_t> ids;
+    rc = survivors(c, ids);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    std::vector<uint64_t> cnt(c->mpuCount);
+    if (c->mpuCount) PSGPU_CHECK(hipMemcpy(cnt.data(), c->counts, (size_t)c->mpuCount * 8, hipMemcpyDeviceToHost));
     memset(stats, 0, sizeof(PsMpuStats) * c->mpuCount);
-    for (uint32_t w = 0; w < W; ++w) {
-        PsMpuStats& s = stats[ids[w] - c->mpuBegin];
+    for (uint32_t m : ids) {
+        PsMpuStats& s = stats[m - c->mpuBegin];
         s.passedPrecheck = 1;
         s.ctFieldEvals = 128;
-        s.ctVertices = (uint32_t)cnt[w];
-        s.ctTriangles = (uint32_t)(cnt[w] >> 32);
+    }
+    for (uint32_t l = 0; l < c->mpuCount; ++l) {
+        stats[l].ctVertices = (uint32_t)cnt[l];
+        stats[l].ctTriangles = (uint32_t)(cnt[l] >> 32);
     }
     return PSGPU_RET_SUCCESS;
 }
-
 int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt) {
     PsMeshInfo I;
     int rc = psgpu_finish(c, &I);
@@ -869,10 +897,13 @@ int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t
     if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
     if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
     if (!mpus) return PSGPU_RET_PARAM_ERROR;
-    const size_t V = I.ctVertices, T = I.ctTriangles, W = I.ctPassedPrecheck;
+    const size_t V = I.ctVertices, T = I.ctTriangles, N = c->mpuCount;
     std::vector<float> pos(V * 3), nrm(V * 3), col(V * 3);
-    std::vector<uint32_t> tris(T * 3), ids(W), voff(W + 1), toff(W + 1);
-    rc = psgpu_download_mesh(c, pos.data(), nrm.data(), col.data(), tris.data(), ids.data(), voff.data(), toff.data());
+    std::vector<uint32_t> tris(T * 3), ids;
+    std::vector<uint64_t> off(N + 1);
+    rc = psgpu_download_mesh(c, pos.data(), nrm.data(), col.data(), tris.data(), off.data());
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    rc = survivors(c, ids);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
     for (uint32_t l = 0; l < c->mpuCount; ++l) {  // Polygonize :360-371
@@ -886,11 +917,11 @@ int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t
         M.ctTriangles = 0;
         M.ctFieldEvals = 0;
     }
-    for (size_t w = 0; w < W; ++w) {
-        PsMPU& M = mpus[ids[w] - c->mpuBegin];
-        const uint32_t v0 = voff[w], nv = voff[w + 1] - v0;
-        const uint32_t t0 = toff[w], nt = toff[w + 1] - t0;
-        M.ctFieldEvals = 128;
+    for (uint32_t m : ids) mpus[m - c->mpuBegin].ctFieldEvals = 128;
+    for (size_t l = 0; l < N; ++l) {
+        PsMPU& M = mpus[l];
+        const uint32_t v0 = (uint32_t)off[l], nv = (uint32_t)off[l + 1] - v0;
+        const uint32_t t0 = (uint32_t)(off[l] >> 32), nt = (uint32_t)(off[l + 1] >> 32) - t0;
         M.ctVertices = (uint16_t)nv;
         M.ctTriangles = (uint16_t)nt;
         memcpy(M.vPos, &pos[(size_t)v0 * 3], (size_t)nv * 12);

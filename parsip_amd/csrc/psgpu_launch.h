@@ -13,14 +13,10 @@ size_t walk_lds_bytes(uint32_t slots);
 size_t precheck_lds_bytes(uint32_t slots);
 hipError_t launch_precheck(const Params& p, hipStream_t s);
 hipError_t launch_mpu(const Params& p, hipStream_t s);
+hipError_t launch_scan(const Params& p, hipStream_t s);
 hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks);
 hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks);
 hipError_t launch_probe(const Params& p, hipStream_t s, const float* xyz, float* out, float* col, uint32_t n,
                         int mode);
-
-// rocPRIM device-wide primitives (psgpu_scan.hip); temp == nullptr queries `bytes`.
-hipError_t select_passing(void* temp, size_t& bytes, const uint8_t* flags, uint32_t begin, uint32_t* out,
-                          uint32_t* count, uint32_t n, hipStream_t s);
-hipError_t scan_counts(void* temp, size_t& bytes, const uint64_t* counts, uint64_t* offs, uint32_t n, hipStream_t s);
 
 }  // namespace psgpu

@@ -25,6 +25,7 @@ typedef unsigned short uint16_t;
 typedef unsigned int uint32_t;
 typedef int int32_t;
 typedef unsigned long long uint64_t;
+typedef long long int64_t;
 #else
 #include <stdint.h>
 #include <hip/hip_runtime.h>
@@ -118,7 +119,7 @@ struct DevModel {
 };
 
 // Compact-mesh work records written by the MPU kernel.
-struct VertexRec {       // 16 B: surface-MPU slot, global MPU id, local vertex id, edge key
+struct VertexRec {       // 16 B: MPU slot in the range, global MPU id, local vertex id, edge key
     uint32_t w;
     uint32_t m;
     uint32_t vidKey;     // vid | key << 16, key = sx | sy<<3 | sz<<6 | axis<<9
@@ -132,17 +133,24 @@ struct TriRec {          // 16 B
 };
 
 // Device-side scalars of one polygonization.
-// Work records are appended to kShards independent queues (shard = slot & 63) so that
-// no single counter takes one returning atomic per MPU (a single word saturates at
-// about 88 atomics/us on MI355X: MI355X_MICROARCH.md 'dequeue').
+// Work records are appended to kShards independent queues so that no single counter
+// takes one returning atomic per MPU (a single word saturates at about 88 atomics/us
+// on MI355X: MI355X_MICROARCH.md 'dequeue').
 constexpr int kShards = 64;
+constexpr uint32_t kScanItems = 8192;   // k_scan: counts per block per chunk (1024 x 8)
+constexpr uint32_t kScanMaxBlocks = 256;
+struct ShardCtr {           // one 128-B line per shard: atomics on one line serialise
+    uint32_t p;             // S1 survivors appended
+    uint32_t v;             // vertex records appended
+    uint32_t t;             // triangle records appended
+    uint32_t s;             // surface MPUs (>= 1 triangle)
+    uint32_t pad[28];
+};
 struct DevCounters {
-    uint32_t passCount;      // MPUs that passed S1
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
-    uint32_t pad[2];
-    uint32_t vShard[kShards];  // vertices appended per shard
-    uint32_t tShard[kShards];  // triangles appended per shard
-    uint32_t sShard[kShards];  // surface MPUs (>= 1 triangle) per shard
+    uint32_t error;          // protocol errors (bit 0: k_scan look-back timeout)
+    uint32_t pad[30];
+    ShardCtr shard[kShards];
 };
 
 // Kernel arguments of one polygonization (one struct, passed by value).
@@ -156,10 +164,15 @@ struct Params {
     uint32_t mpuBegin;
     uint32_t mpuCount;
     uint32_t cull;      // exact per-wave primitive culling enabled
-    uint8_t* passFlags;     // mpuCount (rounded up to 32): S1 outcome per MPU
-    uint32_t* passList;     // mpuCount, global MPU ids of the S1 survivors, ascending
-    uint64_t* counts;       // mpuCount, V | T << 32 per passing slot (zeroed per run)
-    uint64_t* offs;         // mpuCount + 1, exclusive scan of counts (V | T << 32)
+    uint32_t preBlocks;     // k_precheck blocks (32 MPUs each)
+    uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
+    uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
+    uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
+    uint64_t* offs;         // mpuCount + 1: exclusive scan of counts
+    uint64_t* scanStatus;   // k_scan look-back words of this run (zeroed by the previous run)
+    uint64_t* scanStatusNext;
+    uint32_t scanBlocks;    // k_scan blocks
+    uint32_t scanChunks;    // kScanItems chunks per k_scan block
     VertexRec* vq;          // kShards queues of vShardCap records
     uint32_t vShardCap;
     TriRec* tq;             // kShards queues of tShardCap records
@@ -168,8 +181,9 @@ struct Params {
     float* nrm;
     float* col;
     uint32_t* tris;
-    DevCounters* ctr;
-    uint32_t* dequeue;      // [2] work counters for k_vertex / k_tris
+    DevCounters* ctr;       // this run's counters (two sets alternate between runs)
+    DevCounters* ctrNext;   // the next run's, reset by k_finish
+    DevCounters* hostCtr;   // host-mapped copy written by k_finish
     uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
     uint32_t debug;         // ablation switches for profiling (0 in production)
 };

@@ -34,7 +34,7 @@ class PsMeshInfo(ctypes.Structure):
 
 
 class PsMeshDevice(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "nrm", "col", "tris", "surfaceMpuIds", "mpuOffsets")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "nrm", "col", "tris", "mpuOffsets")]
 
 
 EXPORTED_SYMBOLS = [
@@ -75,7 +75,7 @@ def load(build_if_missing: bool = True):
         "psgpu_polygonize": ([vp, f32, u32, u32, vp], i32),
         "psgpu_finish": ([vp, ctypes.POINTER(PsMeshInfo)], i32),
         "psgpu_mesh_device": ([vp, ctypes.POINTER(PsMeshDevice)], i32),
-        "psgpu_download_mesh": ([vp, vp, vp, vp, vp, vp, vp, vp], i32),
+        "psgpu_download_mesh": ([vp, vp, vp, vp, vp, vp], i32),
         "psgpu_download_stats": ([vp, vp], i32),
         "psgpu_export_polympus": ([vp, vp, u32, ctypes.POINTER(u32)], i32),
         "psgpu_polygonize_mpus": ([vp, f32, vp, vp, vp, vp, u32, ctypes.POINTER(u32), vp], i32),
@@ -148,9 +148,8 @@ class Mesh:
     nrm: np.ndarray            # (V,3) f32
     col: np.ndarray            # (V,3) f32
     tris: np.ndarray           # (T,3) u32 global vertex ids
-    surface_mpus: np.ndarray   # (W,) u32 global MPU id of every S1 survivor, ascending
-    vertex_offsets: np.ndarray  # (W+1,)
-    triangle_offsets: np.ndarray  # (W+1,)
+    vertex_offsets: np.ndarray  # (ctMPUs+1,) per MPU of the processed range
+    triangle_offsets: np.ndarray  # (ctMPUs+1,)
 
     def local_tris(self) -> np.ndarray:
         """Triangles with MPU-local (U16) ids, as stored in MPU::triangles."""
@@ -215,18 +214,15 @@ class Polygonizer:
 
     def download(self) -> Mesh:
         info = self.finish()
-        V, T, W = info.ctVertices, info.ctTriangles, info.ctPassedPrecheck
+        V, T, N = info.ctVertices, info.ctTriangles, info.ctMPUs
         pos = np.zeros((V, 3), np.float32)
         nrm = np.zeros((V, 3), np.float32)
         col = np.zeros((V, 3), np.float32)
         tris = np.zeros((T, 3), np.uint32)
-        ids = np.zeros(W, np.uint32)
-        voff = np.zeros(W + 1, np.uint32)
-        toff = np.zeros(W + 1, np.uint32)
+        off = np.zeros(N + 1, np.uint64)
         _check(self._L.psgpu_download_mesh(self._ctx, pos.ctypes.data, nrm.ctypes.data, col.ctypes.data,
-                                           tris.ctypes.data, ids.ctypes.data, voff.ctypes.data,
-                                           toff.ctypes.data), "psgpu_download_mesh")
-        return Mesh(pos, nrm, col, tris, ids, voff, toff)
+                                           tris.ctypes.data, off.ctypes.data), "psgpu_download_mesh")
+        return Mesh(pos, nrm, col, tris, (off & 0xFFFFFFFF).astype(np.int64), (off >> 32).astype(np.int64))
 
     def stats(self) -> np.ndarray:
         info = self.finish()

@@ -26,6 +26,8 @@ def assert_mesh_matches(gmesh, gstats, omesh, normals_atol: float | None = None,
     np.testing.assert_array_equal(gstats["ctFieldEvals"], ost[:, 1], err_msg="ctFieldEvals")
     np.testing.assert_array_equal(gstats["ctVertices"], ost[:, 2], err_msg="per-MPU vertex counts")
     np.testing.assert_array_equal(gstats["ctTriangles"], ost[:, 3], err_msg="per-MPU triangle counts")
+    np.testing.assert_array_equal(gmesh.vertex_offsets, omesh.vertex_offsets, err_msg="per-MPU vertex offsets")
+    np.testing.assert_array_equal(gmesh.triangle_offsets, omesh.triangle_offsets, err_msg="per-MPU triangle offsets")
     assert gmesh.pos.shape == omesh.pos.shape
     assert gmesh.tris.shape == omesh.tris.shape
     np.testing.assert_array_equal(gmesh.local_tris(), omesh.tris, err_msg="triangles (MPU-local ids)")
