@@ -77,6 +77,25 @@ class Group:
         return [o.tolist() for o in out]
 
 
+def measured_traffic(kernel: str, jit: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/<round>_traffic.json, made by tools/gpu_round.sh + tools/traffic.py on the
+    same workload): 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE.  None if absent."""
+    import glob
+
+    names = [f"jit_{kernel[2:]}" if jit else f"psgpu::{kernel}", kernel]
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                ks = json.load(f)["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for n in names:
+            if n in ks and "traffic_bytes" in ks[n]:
+                return ks[n]["traffic_bytes"], os.path.basename(path)
+    return None, None
+
+
 def cpu_baseline(model, cs, n_cells):
     """The oracle (CPU restatement, 'port') on the host's cores: bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -165,6 +184,7 @@ def main():
     dom_flops = kernel_evals.get(dom, evals) * per_eval
     achieved = dom_flops / (kt[dom] * 1e-3) / 1e12
     counts = grp.allgather([info.ctVertices, info.ctTriangles])
+    traffic, traffic_src = measured_traffic(dom, args.jit) if args.config == "C3" else (None, None)
 
     out = {
         "metric": "Mcells/sec polygonized, 256^3 grid 32-prim BlobTree, at 1/2/4/8 MI355X",
@@ -188,7 +208,9 @@ def main():
                    else "interpreter (jit unavailable)", "set_model_s": round(t_model, 3)},
         "roofline": {"bound": "mfma", "pipe": "fp32 VALU (peak = FP32 vector = FP32 MFMA rate)",
                      "kernel": dom, "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / VALU_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
+                     "traffic": None if traffic is None else round(traffic),
+                     "traffic_source": traffic_src,
                      "kernel_ms": round(kt[dom], 4), "ops_per_eval": per_eval,
                      "evals_per_launch": kernel_evals.get(dom, evals)},
         "kernel_ms": {k: round(v, 4) for k, v in kt.items()},

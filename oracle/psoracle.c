@@ -8,10 +8,14 @@
  * includes the legacy TBB headers tbb/blocked_range.h, tbb/parallel_for.h,
  * tbb/enumerable_thread_specific.h, tbb/task_scheduler_observer.h and uses
  * tbb_thread; none are installed, and stand-ins are not permitted), and the
- * reference ships no tests, fixtures or golden vectors for this path.  This
- * restatement is therefore "parity unpinned" except for the marching-cubes table,
- * whose generated contents are pinned to the reference's _CellConfigTable.h by a
- * committed digest (tests/golden/tritable.json).
+ * reference ships no tests, fixtures or golden vectors for this path.  The
+ * restatement is pinned (tests/test_oracle.py) by (1) the outputs the compiled
+ * reference produced in the survey (MPU / S1 / vertex /
+ * triangle counts and per-MPU maxima for C1, C2 and C3 on std::mt19937(42) inputs,
+ * tests/golden/reference_probe.json), which it reproduces exactly, and (2) the
+ * marching-cubes table digest of _CellConfigTable.h (tests/golden/tritable.json).
+ * Bits of positions / normals / colours beyond those counts were never recorded
+ * from the reference: for them the restatement is "parity unpinned".
  *
  * Semantics are restated literally, 4 SSE lanes at a time, so the op-box pruning
  * that the reference decides per 4-lane group (PS_Polygonizer.cpp:1228-1252) is

@@ -2,8 +2,8 @@
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this
 module, and only as the checker / the CPU baseline -- never as the product path.
-Parity status: see psoracle.c (reference unbuildable here; parity unpinned except
-for the marching-cubes table digest).
+Parity status: see psoracle.c (reference unbuildable here; pinned to the reference's
+recorded C1/C2/C3 counts and its marching-cubes table; vertex bits "parity unpinned").
 """
 from __future__ import annotations
 

@@ -124,3 +124,23 @@ def test_jit_compiles_c3(mode):
     """hiprtc specialisation of the C3 tree compiles for gfx950 without a device."""
     m, _, _ = synth.make_config("C3")
     assert gpu.jit_compile(m, mode) > 10000
+
+
+def test_cpp_shim_compiles_and_runs(tmp_path):
+    """include/parsip_gpu.hpp against caller-side SoA types: host-only entry points work
+    and Polygonize fails loudly (-6) without a device, or reports the too-small
+    PolyMPUs capacity (-4) with one."""
+    import shutil
+    import subprocess
+
+    gpp = shutil.which("g++")
+    if gpp is None:
+        pytest.skip("no g++")
+    gpu.load()
+    exe = tmp_path / "shim_check"
+    lib_dir = os.path.join(ROOT, "parsip_amd")
+    subprocess.run([gpp, "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "shim_check.cpp"), "-L", lib_dir, "-l:libparsip_gpu.so",
+                    f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
