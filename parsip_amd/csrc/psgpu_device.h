@@ -481,22 +481,31 @@ __device__ __forceinline__ void mpu_origin(const Params& p, uint32_t m, float o[
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wave_incl_scan(v), 63); }
 
 // S1: 8 corners per MPU, lanes 0-3 z = lo, lanes 4-7 z = lo + side; (x,y) lanes
-// (0,0),(1,0),(0,1),(1,1) (PS_Polygonizer.cpp:488-519).  256 threads = 32 MPUs.
-// Failing MPUs get count 0 here; survivors are appended to the sharded queue pq (one
-// atomic per wave; waves [s*K, (s+1)*K) with K = ceil(waves / 64) append to shard s,
-// so a shard holds at most 8K = pShardCap ids).  k_mpu takes them in any order: the mesh
-// order comes from k_scan over the per-MPU counts.
+// (0,0),(1,0),(0,1),(1,1) (PS_Polygonizer.cpp:488-519).  One wavefront = one 2x2x2
+// brick of MPUs (lanes 8g..8g+7: MPU g = bx*4 + by*2 + bz), so the wave's culling box
+// is compact.  Failing MPUs get count 0 here; survivors are appended to the sharded
+// queue pq (one atomic per wave; waves [s*K, (s+1)*K) with K = pShardCap / 8 append to
+// shard s, so a shard cannot overflow).  k_mpu takes them in any order: the mesh order
+// comes from k_scan over the per-MPU counts.
 template <class EV>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
-    const uint32_t local = blockIdx.x * 32u + (threadIdx.x >> 3);
-    const bool valid = local < p.mpuCount;
-    const uint32_t m = p.mpuBegin + (valid ? local : 0);
+    const uint32_t W = blockIdx.x * 4u + (uint32_t)wave;
+    const uint32_t bzN = p.brickDims[2], byN = p.brickDims[1];
+    const uint32_t nBricks = p.brickDims[0] * byN * bzN;
+    const uint32_t g = (uint32_t)lane >> 3;
+    const uint32_t mi = 2u * (p.brickI0 + W / (byN * bzN)) + ((g >> 2) & 1u);
+    const uint32_t mj = 2u * ((W / bzN) % byN) + ((g >> 1) & 1u);
+    const uint32_t mk = 2u * (W % bzN) + (g & 1u);
+    const uint32_t mg = (mi * p.dims[1] + mj) * p.dims[2] + mk;
+    const bool valid = W < nBricks && mi < p.dims[0] && mj < p.dims[1] && mk < p.dims[2] && mg >= p.mpuBegin &&
+                       mg - p.mpuBegin < p.mpuCount;
+    const uint32_t m = valid ? mg : p.mpuBegin;
     float o[3];
     mpu_origin(p, m, o);
-    const int c = threadIdx.x & 7;
+    const int c = lane & 7;
     const float X = (float)(c & 1), Y = (float)((c >> 1) & 1), Z = (float)(c >> 2);
     const float px = X * p.side + o[0];
     const float py = Y * p.side + o[1];
@@ -506,33 +515,34 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const uint64_t bal = ballot(valid && f > 0.0f);
     uint32_t flags8 = 0;  // bit g: MPU of lanes 8g..8g+7 passed
 #pragma unroll
-    for (int g = 0; g < 8; ++g) flags8 |= (((bal >> (8 * g)) & 0xffull) != 0ull ? 1u : 0u) << g;
-    const uint32_t mine = blockIdx.x * 32u + (uint32_t)wave * 8u + (uint32_t)lane;  // lanes 0..7: MPU g = lane
+    for (int q = 0; q < 8; ++q) flags8 |= (((bal >> (8 * q)) & 0xffull) != 0ull ? 1u : 0u) << q;
+    // lane g < 8 speaks for MPU g (its values are those of lane 8g)
+    const uint32_t mOf = __shfl(m, lane * 8 & 63);
+    const bool vOf = __shfl(valid ? 1 : 0, lane * 8 & 63) != 0;
     const bool pass = lane < 8 && ((flags8 >> lane) & 1u);
-    if (lane < 8 && !pass && mine < p.mpuCount) p.counts[mine] = 0ull;
+    if (lane < 8 && vOf && !pass) p.counts[mOf - p.mpuBegin] = 0ull;
     if (flags8 == 0u) return;
-    // shard = slab of consecutive precheck waves: k_mpu then walks the survivors roughly
-    // in MPU order (neighbouring waves share culling masks and model cache lines)
-    const uint32_t shard = (blockIdx.x * 4u + (uint32_t)wave) / (p.pShardCap / 8u);
+    const uint32_t shard = W / (p.pShardCap / 8u);
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(flags8));
     base = lane_value(base, 0);
-    if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(flags8 & ((1u << lane) - 1u))] = p.mpuBegin + mine;
+    if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(flags8 & ((1u << lane) - 1u))] = mOf;
 }
 
 #ifndef PSGPU_S2_N
 #define PSGPU_S2_N 1  // x-slices per walk in S2 (1, 2, 4 or 8)
 #endif
 constexpr int kLdsFv = 0;
-constexpr int kLdsEdge = 2048;
+constexpr int kLdsEdge = 0;  // edgeVid reuses the field cache: fv is dead after pass 1
 constexpr int kLdsCfg = kLdsEdge + 1536 * 2;
 constexpr int kLdsVbase = kLdsCfg + 344;
 constexpr int kLdsTbase = kLdsVbase + 344 * 2;
 constexpr int kLdsSlots = ((kLdsTbase + 344 * 2) + 15) & ~15;
 
 // Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
-// LDS per block: the packed cube tables (shared), then per wave: fv[512] f32 |
-// edgeVid[1536] u16 | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots.
+// LDS per block: the packed cube tables (shared), then per wave: fv[512] f32 (S2, pass 1)
+// aliased by edgeVid[1536] u16 (passes 2-3; the wavefront fence after pass 1 orders the
+// two) | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots (interpreter).
 constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
 
 template <class EV>

@@ -319,6 +319,8 @@ struct psgpu_ctx {
     bool haveModel = false;
     int cull = 1;
     int debug = 0;
+    int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
+    int finishBlocksPerCU = 4;
     int timing = 0;
     // geometry of the last run
     float cs = 0.0f;
@@ -365,9 +367,26 @@ int hip_fail(hipError_t e, const char* what) {
         if (_e != hipSuccess) return hip_fail(_e, #expr);   \
     } while (0)
 
+// k_precheck covers the MPU range with 2x2x2 bricks of MPUs (one per wavefront: a
+// compact box for its culling test), whole brick rows along x.
+void brick_layout(const psgpu_ctx* c, uint32_t* i0, uint32_t bd[3]) {
+    const uint32_t nyz = c->dims[1] * c->dims[2];
+    const uint32_t first = nyz ? c->mpuBegin / nyz : 0;
+    const uint32_t last = (nyz && c->mpuCount) ? (c->mpuBegin + c->mpuCount - 1) / nyz : first;
+    *i0 = first / 2;
+    bd[0] = c->mpuCount ? last / 2 - first / 2 + 1 : 0;
+    bd[1] = (c->dims[1] + 1) / 2;
+    bd[2] = (c->dims[2] + 1) / 2;
+}
+size_t brick_count(const psgpu_ctx* c) {
+    uint32_t i0, bd[3];
+    brick_layout(c, &i0, bd);
+    return (size_t)bd[0] * bd[1] * bd[2];
+}
+
 int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     const size_t n = std::max<uint32_t>(mpuCount, 1);
-    c->pShardCap = 8u * (uint32_t)(((n + 7) / 8 + kShards - 1) / kShards);
+    c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
     PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
     PSGPU_CHECK(grow(c->offs, c->capOff, n + 1));
@@ -394,7 +413,8 @@ Params make_params(psgpu_ctx* c) {
     p.mpuBegin = c->mpuBegin;
     p.mpuCount = c->mpuCount;
     p.cull = (uint32_t)c->cull;
-    p.preBlocks = (c->mpuCount + 31) / 32;
+    brick_layout(c, &p.brickI0, p.brickDims);
+    p.preBlocks = (uint32_t)((brick_count(c) + 3) / 4);
     p.pq = c->pq;
     p.pShardCap = c->pShardCap;
     p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
@@ -446,7 +466,8 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     Params p = make_params(c);
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool t = c->timing != 0;
-    const uint32_t persist = (uint32_t)c->numCUs * 4;
+    const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
+    const uint32_t persistF = (uint32_t)(c->numCUs * c->finishBlocksPerCU);
     JitKernels* J = c->jit.get();
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
@@ -457,11 +478,11 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     PSGPU_CHECK(launch_scan(p, s));
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-    if (J) PSGPU_CHECK(launch_jit(J->vertex, persist, 256, 0, s, p));
-    else PSGPU_CHECK(launch_vertex(p, s, persist));
+    if (J) PSGPU_CHECK(launch_jit(J->vertex, persistV, 256, 0, s, p));
+    else PSGPU_CHECK(launch_vertex(p, s, persistV));
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
-    if (J) PSGPU_CHECK(launch_jit(J->finish, persist, 256, 0, s, p));
-    else PSGPU_CHECK(launch_finish(p, s, persist));
+    if (J) PSGPU_CHECK(launch_jit(J->finish, persistF, 256, 0, s, p));
+    else PSGPU_CHECK(launch_finish(p, s, persistF));
     if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
     return PSGPU_RET_SUCCESS;
 }
@@ -692,6 +713,8 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
     else if (option == PSGPU_OPT_DEBUG) c->debug = (int)value;
+    else if (option == PSGPU_OPT_VERTEX_BLOCKS_PER_CU && value >= 1 && value <= 32) c->vertexBlocksPerCU = (int)value;
+    else if (option == PSGPU_OPT_FINISH_BLOCKS_PER_CU && value >= 1 && value <= 32) c->finishBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;

@@ -164,7 +164,9 @@ struct Params {
     uint32_t mpuBegin;
     uint32_t mpuCount;
     uint32_t cull;      // exact per-wave primitive culling enabled
-    uint32_t preBlocks;     // k_precheck blocks (32 MPUs each)
+    uint32_t preBlocks;     // k_precheck blocks (4 waves, one 2x2x2 brick of MPUs per wave)
+    uint32_t brickI0;       // first brick row (x) touching the MPU range
+    uint32_t brickDims[3];  // bricks of the range along x, y, z
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)

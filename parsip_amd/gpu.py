@@ -49,6 +49,8 @@ OPT_KERNEL_TIMING = 1
 OPT_CULLING = 2
 OPT_JIT = 3
 OPT_DEBUG = 9
+OPT_VERTEX_BLOCKS_PER_CU = 4
+OPT_FINISH_BLOCKS_PER_CU = 5
 
 
 def load(build_if_missing: bool = True):

@@ -1,9 +1,16 @@
-import csv, collections, sys
+"""Average PMC counter values per kernel over rocprofv3 counter_collection CSVs.
+usage: python tools/pmc_summary.py gpurun_out/<tag>/p*/run_counter_collection.csv"""
+import collections
+import csv
+import sys
+
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in sys.argv[1:]:
-    rows = list(csv.DictReader(open(path)))
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for r in rows:
-        agg[r['Kernel_Name']][r['Counter_Name']].append(float(r['Counter_Value']))
-    for k, d in agg.items():
-        if 'rocclr' in k: continue
-        print(k.split('(')[0][:28], " ".join(f"{c}={sum(v)/len(v):.3e}" for c, v in sorted(d.items())))
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in agg.items():
+    if "rocclr" in k:
+        continue
+    print(k[:40])
+    for c, v in sorted(d.items()):
+        print(f"   {c:28s} {sum(v) / len(v):.4e}")
