@@ -545,6 +545,19 @@ constexpr int kLdsSlots = ((kLdsTbase + 344 * 2) + 15) & ~15;
 // two) | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots (interpreter).
 constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
 
+// Last cell c in [0, 343) with first[c] <= r (first[] = exclusive prefix of per-cell
+// counts, non-decreasing, first[0] = 0, so that cell holds item r): binary lifting,
+// 9 fixed LDS steps.
+__device__ __forceinline__ int find_cell(const uint16_t* first, uint32_t r) {
+    int lo = 0;
+#pragma unroll
+    for (int step = 256; step > 0; step >>= 1) {
+        const int mid = lo + step;
+        if (mid < 343 && (uint32_t)first[mid] <= r) lo = mid;
+    }
+    return lo;
+}
+
 template <class EV>
 __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     const int wave = threadIdx.x >> 6;
@@ -668,56 +681,59 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     __builtin_amdgcn_wave_barrier();
     if (p.debug & 2u) return;  // ablation: pass 1 only
 
-    // pass 2 (:703-808): vertex ids in first-occurrence order of the row, records
-    for (int q = 0; q < 6; ++q) {
-        const int c = q * 64 + lane;
-        if (c >= 343) break;
-        const uint32_t cfg = cellCfg[c];
-        if (cfg == 0 || cfg == 255) continue;
-        const int i = c / 49, j = (c / 7) % 7, k = c % 7;
-        const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
-        const uint64_t order = tab->order[cfg];
-        const int nd = __popc(tab->cross[cfg]);
-        uint32_t vid = cellV[c];
-        for (int r = 0; r < nd; ++r) {
-            const int ed = (int)((order >> (4 * r)) & 15u);
-            if (!((own >> ed) & 1u)) continue;
+    // pass 2 (:703-762), one lane per new vertex r: its cell is the last cell whose first
+    // vertex id is <= r; it is that cell's k-th owned crossing edge in first-occurrence
+    // order of the row, k = r - first id.  Records are written coalesced.
+    for (uint32_t base = 0; base < V; base += 64u) {
+        const uint32_t r = base + (uint32_t)lane;
+        if (r < V) {
+            const int c = find_cell(cellV, r);
+            const uint32_t cfg = cellCfg[c];
+            const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+            const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
+            const uint64_t order = tab->order[cfg];
+            uint32_t left = r - cellV[c];
+            int ed = 0;
+            for (int q = 0; q < 12; ++q) {  // the (left+1)-th owned edge of the row order
+                ed = (int)((order >> (4 * q)) & 15u);
+                if ((own >> ed) & 1u) {
+                    if (left == 0u) break;
+                    --left;
+                }
+            }
             const int eb = (int)((edgeBits >> (5 * ed)) & 31u);
             const int c1 = eb & 7, ax = eb >> 3;
             const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
-            edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)vid;
+            edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
             const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
-            const uint32_t g = qv + vid;
-            if (g < p.vShardCap) vq[g] = VertexRec{w, m, vid | (key << 16), 0u};
-            ++vid;
+            const uint32_t g = qv + r;
+            if (g < p.vShardCap) vq[g] = VertexRec{w, m, r | (key << 16), 0u};
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (p.debug & 4u) return;  // ablation: no triangles
 
-    // pass 3 (S6, :816-825): triangles in table order
-    for (int q = 0; q < 6; ++q) {
-        const int c = q * 64 + lane;
-        if (c >= 343) break;
-        const uint32_t cfg = cellCfg[c];
-        if (cfg == 0 || cfg == 255) continue;
-        const int i = c / 49, j = (c / 7) % 7, k = c % 7;
-        const uint32_t tb = cellT[c];
-        const uint32_t nt = tab->ntri[cfg];
-        const uint64_t row = tab->row[cfg];
-        for (uint32_t t = 0; t < nt; ++t) {
+    // pass 3 (S6, :816-825), one lane per triangle r: its cell (last first-id <= r) and
+    // the (r - first)-th triangle of the cell's table row
+    for (uint32_t base = 0; base < T; base += 64u) {
+        const uint32_t r = base + (uint32_t)lane;
+        if (r < T) {
+            const int c = find_cell(cellT, r);
+            const uint32_t t = r - cellT[c];
+            const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+            const uint64_t row = tab->row[cellCfg[c]];
             uint32_t v[3];
 #pragma unroll
-            for (int s = 0; s < 3; ++s) {
-                const int ed = (int)((row >> (4 * (t * 3 + s))) & 15u);
+            for (int sv = 0; sv < 3; ++sv) {
+                const int ed = (int)((row >> (4 * (t * 3 + sv))) & 15u);
                 const int eb = (int)((edgeBits >> (5 * ed)) & 31u);
                 const int c1 = eb & 7, ax = eb >> 3;
                 const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
-                v[s] = edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax];
+                v[sv] = edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax];
             }
-            const uint32_t g = qt + tb + t;
-            if (g < p.tShardCap) tq[g] = TriRec{w, tb + t, v[0] | (v[1] << 16), v[2]};
+            const uint32_t g = qt + r;
+            if (g < p.tShardCap) tq[g] = TriRec{w, r, v[0] | (v[1] << 16), v[2]};
         }
     }
 }
