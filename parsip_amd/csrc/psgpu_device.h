@@ -259,62 +259,43 @@ __device__ __forceinline__ bool op_colour_weights(uint32_t type, float lf, float
 // ---------------------------------------------------------------------------
 // Exact culling (never changes a bit of output).  A primitive whose support cannot
 // reach any point of the wave has computed dist2 >= 1, i.e. field exactly +0, and
-// is not evaluated.  For the wave's AABB with centre c and half-diagonal h, every
-// point q has d(q) >= d(c) - h for the 1-Lipschitz distances of Point, infinite Line,
-// axis-aligned Cube and the capped Cylinder with |axis| = 1.  The host marks a prim
-// cullable only without a matrix and with finite, well-conditioned parameters;
-// Cylinder also needs the AABB clear of its infinite axis (where the reference's
-// sqrt of a rounded-negative value is NaN).  The margin d^2 >= 1.02 covers fp32
-// rounding of the reference formulas by orders of magnitude.  Triangle is a constant
-// +0 (dist2 = FLT_MAX) and is always culled.
+// is not evaluated.  Every cullable primitive has a skeleton segment (CullSeg) whose
+// distance minus a radius bounds its distance from below and is 1-Lipschitz: Point
+// (a point), infinite Line (an unbounded segment), capped Cylinder with |axis| = 1
+// (its axis segment, radius r), axis-aligned Cube (its centre, radius s*sqrt(3)).  For
+// the wave's AABB with centre c and half-diagonal h every point q then has
+// d(q) >= d(c) - h.  The host marks a prim cullable only without a matrix and with
+// finite, well-conditioned parameters; Cylinder also needs the AABB clear of its
+// infinite axis (where the reference's sqrt of a rounded-negative value is NaN).  The
+// margin d^2 >= 1.02 covers fp32 rounding of the reference formulas by orders of
+// magnitude.  Triangle is a constant +0 (dist2 = FLT_MAX) and is always culled.
 struct CullMask {
     uint64_t lo, hi;
 };
 
-__device__ __forceinline__ float cull_dist(CPrim& P, float cx, float cy, float cz, float* axisDist) {
-    *axisDist = 1e30f;
-    switch (P.type) {
-    case PSGPU_T_POINT: {
-        float dx = cx - P.pos[0], dy = cy - P.pos[1], dz = cz - P.pos[2];
-        return __builtin_amdgcn_sqrtf(dx * dx + dy * dy + dz * dz);
-    }
-    case PSGPU_T_LINE: {
-        float ux = P.dir[0] - P.pos[0], uy = P.dir[1] - P.pos[1], uz = P.dir[2] - P.pos[2];
-        float dx = cx - P.pos[0], dy = cy - P.pos[1], dz = cz - P.pos[2];
-        float uu = ux * ux + uy * uy + uz * uz;
-        float t = (dx * ux + dy * uy + dz * uz) * __builtin_amdgcn_rcpf(uu);
-        float ex = dx - t * ux, ey = dy - t * uy, ez = dz - t * uz;
-        return __builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez);
-    }
-    case PSGPU_T_CYLINDER: {
-        float dx = cx - P.pos[0], dy = cy - P.pos[1], dz = cz - P.pos[2];
-        float yy = dx * P.dir[0] + dy * P.dir[1] + dz * P.dir[2];
-        float rr = dx * dx + dy * dy + dz * dz - yy * yy;
-        float rad = __builtin_amdgcn_sqrtf(rr > 0.0f ? rr : 0.0f);
-        *axisDist = rad;
-        float ex = rad - P.res[0];
-        ex = ex > 0.0f ? ex : 0.0f;
-        float ey = yy < 0.0f ? -yy : (yy > P.res[1] ? yy - P.res[1] : 0.0f);
-        return __builtin_amdgcn_sqrtf(ex * ex + ey * ey);
-    }
-    case PSGPU_T_CUBE: {
-        float s = P.res[0];
-        float d[3] = {cx - P.pos[0], cy - P.pos[1], cz - P.pos[2]};
-        float acc = 0.0f;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            float e = fabsf(d[a]) - s;
-            e = e > 0.0f ? e : 0.0f;
-            acc += e * e;
-        }
-        return __builtin_amdgcn_sqrtf(acc);
-    }
-    default:
-        return 0.0f;
-    }
+// Lower bound of the primitive's distance from c, and (axis clearance) the distance
+// of c from the segment's infinite line.
+__device__ __forceinline__ float cull_dist(const CullSeg& S, uint32_t flags, float cx, float cy, float cz,
+                                           float* lineDist) {
+    const float dx = cx - S.a[0], dy = cy - S.a[1], dz = cz - S.a[2];
+    const float t = (dx * S.u[0] + dy * S.u[1] + dz * S.u[2]) * S.invUU;
+    const float lx = dx - t * S.u[0], ly = dy - t * S.u[1], lz = dz - t * S.u[2];
+    *lineDist = __builtin_amdgcn_sqrtf(lx * lx + ly * ly + lz * lz);
+    const float tc = (flags & 2u) ? t : fminf(fmaxf(t, 0.0f), 1.0f);
+    const float ex = dx - tc * S.u[0], ey = dy - tc * S.u[1], ez = dz - tc * S.u[2];
+    return __builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez) - S.radius;
 }
 
-// Cull mask for an AABB given by wave-uniform bounds.  Lane l tests prims l, l+64.
+__device__ __forceinline__ CullSeg load_cullseg(ModelPtr M, int i) {
+    const CullSeg __attribute__((address_space(4)))& src = M->cull[i];
+    CullSeg S;
+    S.a[0] = src.a[0]; S.a[1] = src.a[1]; S.a[2] = src.a[2];
+    S.u[0] = src.u[0]; S.u[1] = src.u[1]; S.u[2] = src.u[2];
+    S.invUU = src.invUU;
+    S.radius = src.radius;
+    return S;
+}
+
 __device__ __forceinline__ CullMask cull_mask_box(ModelPtr M, float x0, float y0, float z0, float x1, float y1,
                                                   float z1) {
     CullMask cm{0ull, 0ull};
@@ -329,11 +310,13 @@ __device__ __forceinline__ CullMask cull_mask_box(ModelPtr M, float x0, float y0
         bool cull = false;
         if (i < n) {
             CPrim& P = M->prims[i];
-            if (P.cullable) {
-                float ad;
-                const float d = cull_dist(P, cx, cy, cz, &ad) - h;
+            const uint32_t fl = P.cullable;
+            if (fl & 1u) {
+                float ld;
+                const CullSeg S = load_cullseg(M, i);
+                const float d = cull_dist(S, fl, cx, cy, cz, &ld) - h;
                 cull = d > 0.0f && d * d >= 1.02f;
-                if (P.type == PSGPU_T_CYLINDER) cull = cull && (ad - h > 0.05f);
+                if (fl & 4u) cull = cull && (ld - h > 0.05f);
             } else if (P.type == PSGPU_T_TRIANGLE) {
                 cull = true;
             }

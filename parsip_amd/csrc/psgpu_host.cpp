@@ -273,7 +273,28 @@ int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, con
         } break;
         default: c = false; break;
         }
-        d.cullable = c ? 1u : 0u;
+        // culling skeleton (CullSeg, psgpu_model.h): a lower bound of the distance
+        CullSeg& cs = D.cull[i];
+        memset(&cs, 0, sizeof(cs));
+        uint32_t flags = c ? 1u : 0u;
+        if (c) {
+            for (int a = 0; a < 3; ++a) cs.a[a] = d.pos[a];
+            double uu = 0.0;
+            if (d.type == PSGPU_PRIM_LINE) {
+                for (int a = 0; a < 3; ++a) cs.u[a] = d.dir[a] - d.pos[a];
+                flags |= 2u;
+            } else if (d.type == PSGPU_PRIM_CYLINDER) {
+                for (int a = 0; a < 3; ++a) cs.u[a] = d.res[1] * d.dir[a];  // axis segment, length h
+                cs.radius = d.res[0];
+                flags |= 4u;
+            } else if (d.type == PSGPU_PRIM_CUBE) {
+                cs.radius = (float)(d.res[0] * 1.7320508075688772 * (1.0 + 1e-6));
+            }
+            for (int a = 0; a < 3; ++a) uu += (double)cs.u[a] * cs.u[a];
+            cs.invUU = uu > 0.0 ? (float)(1.0 / uu) : 0.0f;
+            if (d.type == PSGPU_PRIM_CYLINDER && uu == 0.0) flags &= ~1u;  // h = 0: no axis direction
+        }
+        d.cullable = flags;
     }
     return PSGPU_RET_SUCCESS;
 }

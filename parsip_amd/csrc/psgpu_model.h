@@ -97,8 +97,8 @@ struct DevPrim {         // 128 B
     float col[3];
     uint32_t type;
     uint32_t hasMatrix;  // idxMatrix != 0
-    uint32_t cullable;   // exact culling bound valid for this prim (see kernels)
-    float cullRadius;    // support radius used by the cull test
+    uint32_t cullable;   // bit 0: exact culling bound valid; 1: unbounded line; 2: axis clearance
+    float cullRadius;    // skeleton-to-surface slack of the bound (cube: half diagonal)
     float mat[12];       // SOABlobPrimMatrices row-major 3x4 (12-float stride)
     float pad[4];
 };
@@ -106,6 +106,16 @@ static_assert(sizeof(DevPrim) == 128, "DevPrim size");
 
 constexpr int kMaxInstr = 512;
 constexpr int kMaxSlots = 64;
+
+// Culling skeleton of a primitive: the segment A + t*U (t in [0,1], or any t for the
+// unbounded Line) whose distance minus cullRadius bounds the primitive's distance
+// from below; one branch-free formula for every type.
+struct CullSeg {         // 32 B
+    float a[3];
+    float u[3];
+    float invUU;         // 1 / |U|^2, 0 for a point
+    float radius;
+};
 
 struct DevModel {
     uint32_t nInstr;
@@ -116,6 +126,7 @@ struct DevModel {
     Instr instr[kMaxInstr];
     DevOp ops[128];
     DevPrim prims[128];
+    CullSeg cull[128];
 };
 
 // Compact-mesh work records written by the MPU kernel.
