@@ -133,7 +133,9 @@ def main():
     args = ap.parse_args()
 
     grp = Group()
-    poly = gpu.Polygonizer(grp.local)  # HIP device initialised before torch is imported
+    # one process per GPU (LOCAL_RANK); PSGPU_BENCH_DEVICE pins every rank to one device
+    # (multi-rank rehearsal on a one-GPU box)
+    poly = gpu.Polygonizer(int(os.environ.get("PSGPU_BENCH_DEVICE", grp.local)))  # HIP before torch
     grp.init()
     if args.no_cull:
         poly.set_option(gpu.OPT_CULLING, 0)

@@ -27,10 +27,15 @@ def main():
     polys = []
     for v in a.variants:
         p = gpu.Polygonizer(0)
+        os.environ.pop("PSGPU_JIT_FLAGS", None)
         for kv in v.split(","):
-            k, val = kv.split("=")
+            k, val = kv.split("=", 1)
+            if k == "flags":  # extra hiprtc flags for this variant's kernels ('+' separates)
+                os.environ["PSGPU_JIT_FLAGS"] = val.replace("+", " ")
+                continue
             p.set_option(OPT[k], int(val))
         p.set_model(model)
+        os.environ.pop("PSGPU_JIT_FLAGS", None)
         p.run(cs)
         polys.append(p)
     kt = {v: {} for v in a.variants}
