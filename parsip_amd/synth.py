@@ -14,6 +14,7 @@ The portable splitmix64 stream of §8(d) (``(u >> 40) * 2**-24``) stays availabl
 * C2  8 prims (2 per type), 7 ops, 128^3 over [-4,4]^3
 * C3 32 prims (8 per type), 31 ops, 256^3 over [-4,4]^3   (the headline workload)
 * C5 64 prims, 63 ops, 512^3 over [-4,4]^3, animated: centre.x += 0.25 sin(2 pi f/60 + i)
+  (C2-C4 animate by the same motion relative to frame 0, which stays the probe tree)
 
 Prims cycle Point, Line (end = start + (0.8, 0.3, 0)), Cylinder (axis (0,1,0), r 0.2,
 h 0.8), Cube (half side 0.3); centres uniform in [-2,2]^3; identity matrices.
@@ -250,6 +251,8 @@ def make_config(name: str, frame: int = 0, seed: int = 42, rng: str = "mt19937")
             c = np.array([draw() for _ in range(3)], np.float32)
             if name == "C5":
                 c[0] = np.float32(c[0] + np.float32(0.25 * math.sin(2.0 * math.pi * frame / 60.0 + i)))
+            elif frame:  # C2-C4 animate the same way but keep frame 0 = the reference-probe tree
+                c[0] = np.float32(c[0] + np.float32(0.25 * (math.sin(2.0 * math.pi * frame / 60.0 + i) - math.sin(i))))
             set_prim(model, i, _CYCLE[i % 4], c)
         model.prims["ctPrims"][0] = n_prims
         build_balanced_ops(model, n_prims)

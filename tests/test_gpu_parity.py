@@ -166,3 +166,16 @@ def test_drop_in_polygonize(gpu_poly, oracle):
     # reference error code for an empty model
     empty = soa.Model.empty()
     assert gpu.Polygonize(cs, empty)[0] == soa.RET_PARAM_ERROR
+
+
+def test_scene_train(gpu_poly, oracle):
+    """The reference's own scene file (95 transformed prims, n-ary ops binarized) through
+    the linearizer: matrices on every primitive, Ricci / Difference / Union / Blend."""
+    from parsip_amd import blobtree, scene
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_corrected.scene")
+    code, model = blobtree.linearize_blobtree(blobtree.binarize(scene.load_scene(path)[0]))
+    assert code == 0
+    gm, gs, om = run_both(gpu_poly, oracle, model, 0.2)
+    assert len(gm.pos) > 10000
+    assert_mesh_matches(gm, gs, om)
