@@ -828,8 +828,8 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         nx = nx * im;
         ny = ny * im;
         nz = nz * im;
-        if (valid && j == 0) {
-            const uint32_t gi = outBase + (R.vidKey & 0xffffu);
+        const uint32_t gi = outBase + (R.vidKey & 0xffffu);
+        if (valid && j == 0 && gi < p.vCap) {  // past vCap: finish() grows and re-runs
             p.pos[gi * 3 + 0] = P0; p.pos[gi * 3 + 1] = P1; p.pos[gi * 3 + 2] = P2;
             p.nrm[gi * 3 + 0] = nx; p.nrm[gi * 3 + 1] = ny; p.nrm[gi * 3 + 2] = nz;
         }
@@ -845,7 +845,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
-    const uint32_t nV = (uint32_t)p.offs[p.mpuCount];
+    const uint32_t nV = min((uint32_t)p.offs[p.mpuCount], p.vCap);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
     if (blockIdx.x == 0) {  // the run's counters for the host (mapped pinned memory)
@@ -882,6 +882,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         const uint64_t o = p.offs[R.w];
         const uint32_t gt = (uint32_t)(o >> 32) + R.tlocal;
         const uint32_t base = (uint32_t)o;
+        if (gt >= p.tCap) continue;  // finish() grows and re-runs
         p.tris[gt * 3 + 0] = base + (R.v01 & 0xffffu);
         p.tris[gt * 3 + 1] = base + (R.v01 >> 16);
         p.tris[gt * 3 + 2] = base + R.v2;

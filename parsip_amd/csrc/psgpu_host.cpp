@@ -453,6 +453,8 @@ Params make_params(psgpu_ctx* c) {
     p.nrm = c->nrm;
     p.col = c->col;
     p.tris = c->tris;
+    p.vCap = c->vcap;
+    p.tCap = c->tcap;
     p.ctr = c->ctr + c->parity;
     p.ctrNext = c->ctr + (c->parity ^ 1u);
     p.hostCtr = c->hostCtrDev;
@@ -734,6 +736,20 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
     else if (option == PSGPU_OPT_DEBUG) c->debug = (int)value;
+    else if (option == PSGPU_OPT_CAPACITY && value >= 64 && value <= (1ll << 30)) {
+        // restart the output / work-queue buffers at this vertex capacity (they grow on demand)
+        if (c->pending) (void)hipStreamSynchronize(c->runStream);
+        void* bufs[] = {c->vq, c->tq, c->pos, c->nrm, c->col, c->tris};
+        for (void* b : bufs)
+            if (b) (void)hipFree(b);
+        c->vq = nullptr; c->tq = nullptr; c->pos = nullptr; c->nrm = nullptr; c->col = nullptr; c->tris = nullptr;
+        c->capVq = c->capTq = c->capV = c->capT = 0;
+        c->vcap = (uint32_t)value;
+        c->tcap = (uint32_t)std::min<int64_t>(2 * value, 0xffffffffll);
+        c->vShardCap = (uint32_t)std::max<int64_t>(16, value / kShards);
+        c->tShardCap = 2 * c->vShardCap;
+        c->haveResult = false;
+    }
     else if (option == PSGPU_OPT_VERTEX_BLOCKS_PER_CU && value >= 1 && value <= 32) c->vertexBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_FINISH_BLOCKS_PER_CU && value >= 1 && value <= 32) c->finishBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_JIT) {

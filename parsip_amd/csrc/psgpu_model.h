@@ -190,10 +190,11 @@ struct Params {
     uint32_t vShardCap;
     TriRec* tq;             // kShards queues of tShardCap records
     uint32_t tShardCap;
-    float* pos;
+    float* pos;             // vCap vertices
     float* nrm;
     float* col;
-    uint32_t* tris;
+    uint32_t* tris;         // tCap triangles
+    uint32_t vCap, tCap;
     DevCounters* ctr;       // this run's counters (two sets alternate between runs)
     DevCounters* ctrNext;   // the next run's, reset by k_finish
     DevCounters* hostCtr;   // host-mapped copy written by k_finish

@@ -51,6 +51,7 @@ OPT_JIT = 3
 OPT_DEBUG = 9
 OPT_VERTEX_BLOCKS_PER_CU = 4
 OPT_FINISH_BLOCKS_PER_CU = 5
+OPT_CAPACITY = 6
 
 
 def load(build_if_missing: bool = True):

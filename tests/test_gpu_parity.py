@@ -179,3 +179,13 @@ def test_scene_train(gpu_poly, oracle):
     gm, gs, om = run_both(gpu_poly, oracle, model, 0.2)
     assert len(gm.pos) > 10000
     assert_mesh_matches(gm, gs, om)
+
+
+@pytest.mark.parametrize("cap", [64, 5000])
+def test_capacity_overflow_regrows(gpu_poly, oracle, cap):
+    """Compact mesh / work queues far too small: kernels must not write past them, and
+    finish() grows the buffers and repeats the run (C5-sized meshes take this path)."""
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_option(gpu.OPT_CAPACITY, cap)
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert_mesh_matches(gm, gs, om)
