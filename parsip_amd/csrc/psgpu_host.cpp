@@ -370,6 +370,13 @@ struct psgpu_ctx {
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
     uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
     hipEvent_t ev[kNumKernels + 1] = {};
+    int useGraph = 0;  // replay repeated launch sequences from a hipGraph (measured slower on ROCm 7.2)
+    struct GraphSlot {
+        hipGraphExec_t exec = nullptr;
+        JitKernels* jit = nullptr;
+        Params key{};
+        uint32_t shape[3] = {0, 0, 0};
+    } graphs[2];
     float lastMs[kNumKernels] = {};
     PsMeshInfo info{};
 };
@@ -422,7 +429,8 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
 }
 
 Params make_params(psgpu_ctx* c) {
-    Params p{};
+    Params p;
+    memset(&p, 0, sizeof(p));  // padding too: graph replay compares parameter bytes
     p.model = c->dModel;
     p.tables = c->dTables;
     p.cs = c->cs;
@@ -470,43 +478,75 @@ hipError_t launch_jit(hipFunction_t f, uint32_t blocks, uint32_t threads, size_t
 
 // One polygonization = 5 kernels, no copies or fills: k_precheck resets the counters,
 // k_finish publishes them to mapped host memory.
-int enqueue(psgpu_ctx* c, hipStream_t s) {
-    if (c->mpuCount == 0) {
-        memset(c->hostCtr, 0, sizeof(DevCounters));
-    c->hostCtr->firstOverflow = 0x7fffffff;
-    {
-        DevCounters init[2];
-        memset(init, 0, sizeof(init));
-        init[0].firstOverflow = init[1].firstOverflow = 0x7fffffff;
-        if (hipMemcpy(c->ctr, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) {
-            psgpu_destroy(c);
-            return PSGPU_RET_DEVICE_ERROR;
-        }
-    }
-        c->hostCtr->firstOverflow = 0x7fffffff;
-        return PSGPU_RET_SUCCESS;
-    }
-    Params p = make_params(c);
-    c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
-    const bool t = c->timing != 0;
+// The five launches of one polygonization (shared by direct launch and graph capture).
+int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
+    Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
     const uint32_t persistF = (uint32_t)(c->numCUs * c->finishBlocksPerCU);
     JitKernels* J = c->jit.get();
-    if (t) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
-    if (t) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
     if (J) PSGPU_CHECK(launch_jit(J->mpu, kShards * ((p.pShardCap + 3) / 4), 256, mpu_lds_bytes(0), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
-    if (t) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     PSGPU_CHECK(launch_scan(p, s));
-    if (t) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
     if (J) PSGPU_CHECK(launch_jit(J->vertex, persistV, 256, 0, s, p));
     else PSGPU_CHECK(launch_vertex(p, s, persistV));
-    if (t) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
     if (J) PSGPU_CHECK(launch_jit(J->finish, persistF, 256, 0, s, p));
     else PSGPU_CHECK(launch_finish(p, s, persistF));
-    if (t) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
+    return PSGPU_RET_SUCCESS;
+}
+
+void drop_graphs(psgpu_ctx* c) {
+    for (auto& g : c->graphs) {
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        g = psgpu_ctx::GraphSlot{};
+    }
+}
+
+// One polygonization = 5 kernels, no copies or fills: k_precheck needs nothing reset
+// (k_finish of the previous run reset this run's counters) and k_finish publishes the
+// counters to mapped host memory.  Replayed from a hipGraph (one per counter set) while
+// the launch parameters repeat, e.g. per frame of an animation.
+int enqueue(psgpu_ctx* c, hipStream_t s) {
+    if (c->mpuCount == 0) {  // nothing to launch: an empty result
+        memset(c->hostCtr, 0, sizeof(DevCounters));
+        c->hostCtr->firstOverflow = 0x7fffffff;
+        return PSGPU_RET_SUCCESS;
+    }
+    const Params p = make_params(c);
+    const uint32_t slot = c->parity;
+    c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
+    const bool timed = c->timing != 0;
+    if (!c->useGraph || timed || s == nullptr) return launch_all(c, p, s, timed);
+    psgpu_ctx::GraphSlot& g = c->graphs[slot];
+    const uint32_t shape[3] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs};
+    if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
+          memcmp(g.shape, shape, sizeof(shape)) == 0)) {
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        g = psgpu_ctx::GraphSlot{};
+        hipGraph_t graph = nullptr;
+        PSGPU_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        const int rc = launch_all(c, p, s, false);
+        const hipError_t ec = hipStreamEndCapture(s, &graph);
+        if (rc != PSGPU_RET_SUCCESS) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        PSGPU_CHECK(ec);
+        const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        PSGPU_CHECK(ei);
+        g.key = p;
+        g.jit = c->jit.get();
+        memcpy(g.shape, shape, sizeof(shape));
+    }
+    PSGPU_CHECK(hipGraphLaunch(g.exec, s));
     return PSGPU_RET_SUCCESS;
 }
 
@@ -719,6 +759,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    drop_graphs(c);
     c->jit.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->offs, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr};
@@ -736,6 +777,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
     else if (option == PSGPU_OPT_DEBUG) c->debug = (int)value;
+    else if (option == PSGPU_OPT_GRAPH) c->useGraph = value != 0;
     else if (option == PSGPU_OPT_CAPACITY && value >= 64 && value <= (1ll << 30)) {
         // restart the output / work-queue buffers at this vertex capacity (they grow on demand)
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
@@ -755,6 +797,8 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;
+        if (c->pending) (void)hipStreamSynchronize(c->runStream);
+        drop_graphs(c);
         if (!c->useJit) c->jit.reset();
         else if (c->haveModel) {
             c->jit = jit_get(c->model, c->useJit == 2, c->device, &c->jitError);
@@ -774,6 +818,7 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     rc = build_device_model(*prims, *mats, *ops, *m);
     if (rc != PSGPU_RET_SUCCESS) { delete m; return rc; }
     if (c->pending) (void)hipStreamSynchronize(c->runStream);
+    drop_graphs(c);  // captured launches may name the old specialised kernels
     c->model = *m;
     delete m;
     memcpy(&c->primsHost, prims, sizeof(PsSoaBlobPrims));

@@ -189,3 +189,16 @@ def test_capacity_overflow_regrows(gpu_poly, oracle, cap):
     gpu_poly.set_option(gpu.OPT_CAPACITY, cap)
     gm, gs, om = run_both(gpu_poly, oracle, model, cs)
     assert_mesh_matches(gm, gs, om)
+
+
+def test_graph_replay_and_frames(gpu_poly, oracle):
+    """hipGraph replay of the launch sequence across model updates of one structure
+    (an animation: C2 frames 0..3), each frame bit-exact to the oracle."""
+    gpu_poly.set_option(gpu.OPT_GRAPH, 1)
+    try:
+        for f in range(4):
+            model, cs, _ = synth.make_config("C2", frame=f)
+            gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+            assert_mesh_matches(gm, gs, om)
+    finally:
+        gpu_poly.set_option(gpu.OPT_GRAPH, 0)
