@@ -818,7 +818,8 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     rc = build_device_model(*prims, *mats, *ops, *m);
     if (rc != PSGPU_RET_SUCCESS) { delete m; return rc; }
     if (c->pending) (void)hipStreamSynchronize(c->runStream);
-    drop_graphs(c);  // captured launches may name the old specialised kernels
+    // captured graphs stay valid: specialised modules live as long as the process
+    // (jit_get's cache) and the replay key compares the kernels and every parameter
     c->model = *m;
     delete m;
     memcpy(&c->primsHost, prims, sizeof(PsSoaBlobPrims));
