@@ -202,3 +202,24 @@ def test_graph_replay_and_frames(gpu_poly, oracle):
             assert_mesh_matches(gm, gs, om)
     finally:
         gpu_poly.set_option(gpu.OPT_GRAPH, 0)
+
+
+def test_c5_animation_frame(gpu_poly, oracle):
+    """The 512^3, 64-primitive animated workload (C5), one frame against the oracle."""
+    model, cs, _ = synth.make_config("C5", frame=7)
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert len(gm.pos) > 1_000_000
+    assert_mesh_matches(gm, gs, om)
+
+
+def test_animation_driver(gpu_poly, oracle):
+    from parsip_amd import animate
+
+    seen = []
+    anim = animate.Animation(gpu_poly, lambda f: synth.make_config("C2", frame=f)[0], synth.make_config("C2")[1])
+    out = anim.run(3, sink=lambda f, mesh: seen.append((f, len(mesh.pos))), download=True)
+    gpu_poly.set_option(gpu.OPT_GRAPH, 0)
+    assert out["frames"] == 3 and [f for f, _ in seen] == [0, 1, 2]
+    model, cs, _ = synth.make_config("C2", frame=2)
+    om = oracle.polygonize(model, cs, threads=8)
+    assert seen[2][1] == len(om.pos)
