@@ -493,8 +493,14 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const float px = X * p.side + o[0];
     const float py = Y * p.side + o[1];
     const float pz = Z * p.side + o[2];
-    const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
-    const float f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
+    float f = -1.0f;
+    if (!(p.debug & 8u)) {  // ablation bit 3: S1 without the walk (nothing passes)
+        const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+        f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
+    } else if (p.debug & 16u) {  // bit 4: the culling mask only
+        const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+        f = (float)(cm.lo & 1ull) - 1.0f;
+    }
     const uint64_t bal = ballot(valid && f > 0.0f);
     uint32_t flags8 = 0;  // bit g: MPU of lanes 8g..8g+7 passed
 #pragma unroll
