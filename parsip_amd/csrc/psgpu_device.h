@@ -469,7 +469,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wav
 // is compact.  Failing MPUs get count 0 here; survivors are appended to the sharded
 // queue pq (one atomic per wave; waves [s*K, (s+1)*K) with K = pShardCap / 8 append to
 // shard s, so a shard cannot overflow).  k_mpu takes them in any order: the mesh order
-// comes from k_scan over the per-MPU counts.
+// comes from the scan of the per-MPU counts (in k_vertex).
 template <class EV>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
@@ -696,7 +696,10 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
             edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
             const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
             const uint32_t g = qv + r;
-            if (g < p.vShardCap) vq[g] = VertexRec{w, m, r | (key << 16), 0u};
+            if (g < p.vShardCap) {
+                vq[g].w = w;
+                vq[g].vidKey = r | (key << 16);
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -749,6 +752,161 @@ struct ShardBatches {
     }
 };
 
+// Exclusive offsets of the per-MPU (V | T << 32) counts of the range, in MPU order (the
+// reference's PolyMPUs order): offs[0] = 0, offs[w + 1] = inclusive sum.  Single pass,
+// run by the first scanBlocks 256-thread blocks of k_vertex (all co-resident): each owns
+// chunks of kScanItems counts (8 consecutive per thread, 64-B vector loads), publishes
+// its aggregate, looks back over up to 64 predecessors at once (decoupled look-back),
+// then scans.  V and T halves are scanned as two u32 DPP
+// scans (their totals stay below 2^31).  Status words (state << 62 | T << 31 | V) start
+// at zero: the previous run's k_finish cleared them.  All blocks are resident.
+__device__ __forceinline__ uint64_t scan_word(uint32_t state, uint32_t v, uint32_t t) {
+    return ((uint64_t)state << 62) | ((uint64_t)(t & 0x7fffffffu) << 31) | (uint64_t)(v & 0x7fffffffu);
+}
+
+struct Chunk8 {
+    uint64_t c[8];
+    __device__ void load(const uint64_t* counts, uint32_t e, uint32_t hi) {
+        if (e + 8 <= hi) {
+            const uint4* src = reinterpret_cast<const uint4*>(counts + e);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint4 q = src[i];
+                c[2 * i] = (uint64_t)q.x | ((uint64_t)q.y << 32);
+                c[2 * i + 1] = (uint64_t)q.z | ((uint64_t)q.w << 32);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = e + i < hi ? counts[e + i] : 0ull;
+        }
+    }
+    __device__ void sum(uint32_t& v, uint32_t& t) const {
+        v = 0u;
+        t = 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            v += (uint32_t)c[i];
+            t += (uint32_t)(c[i] >> 32);
+        }
+    }
+};
+
+__device__ __forceinline__ void scan_counts_block(const Params& p, uint32_t b) {
+    constexpr int kWaves = (int)(kScanItems / 512u);
+    __shared__ uint32_t sWave[2][kWaves];
+    __shared__ uint32_t sPrefix[2];
+    const uint32_t n = p.mpuCount;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t lo = b * p.scanChunks * kScanItems;
+    const uint32_t hi = min(n, lo + p.scanChunks * kScanItems);
+    // pass 1: the block's aggregate (the first chunk stays in registers)
+    Chunk8 ch;
+    ch.load(p.counts, lo + (uint32_t)t * 8u, hi);
+    uint32_t sv, st;
+    ch.sum(sv, st);
+    for (uint32_t c = 1; c < p.scanChunks; ++c) {
+        Chunk8 more;
+        more.load(p.counts, lo + c * kScanItems + (uint32_t)t * 8u, hi);
+        uint32_t a, bb;
+        more.sum(a, bb);
+        sv += a;
+        st += bb;
+    }
+    const uint32_t wv_v = lane_value(wave_incl_scan(sv), 63), wv_t = lane_value(wave_incl_scan(st), 63);
+    if (lane == 0) {
+        sWave[0][wv] = wv_v;
+        sWave[1][wv] = wv_t;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        uint32_t aggV = 0u, aggT = 0u;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            aggV += sWave[0][w];
+            aggT += sWave[1][w];
+        }
+        uint32_t exV = 0u, exT = 0u;
+        if (b == 0) {
+            if (lane == 0) __hip_atomic_store(&p.scanStatus[0], scan_word(2, aggV, aggT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(&p.scanStatus[b], scan_word(1, aggV, aggT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t)b - 1;
+            for (;;) {
+                const int64_t idx = j - lane;
+                uint32_t state = 2, v = 0u, tt = 0u;
+                if (idx >= 0) {
+                    uint64_t w = 0ull;
+                    uint32_t spins = 0;  // bounded: a broken protocol ends the kernel, flagged
+                    do {
+                        w = __hip_atomic_load(&p.scanStatus[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } while ((w >> 62) == 0ull && ++spins < (1u << 20));
+                    if ((w >> 62) == 0ull) {
+                        atomicOr(&p.ctr->error, 1u);
+                        w = scan_word(2, 0u, 0u);
+                    }
+                    state = (uint32_t)(w >> 62);
+                    v = (uint32_t)(w & 0x7fffffffull);
+                    tt = (uint32_t)((w >> 31) & 0x7fffffffull);
+                }
+                const uint64_t inc = ballot(state == 2);
+                const bool stop = inc != 0ull;
+                const int k = stop ? __builtin_ctzll(inc) : 63;  // newest predecessor with an inclusive prefix
+                exV += lane_value(wave_incl_scan(lane <= k ? v : 0u), 63);
+                exT += lane_value(wave_incl_scan(lane <= k ? tt : 0u), 63);
+                if (stop) break;
+                j -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&p.scanStatus[b], scan_word(2, exV + aggV, exT + aggT), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            sPrefix[0] = exV;
+            sPrefix[1] = exT;
+        }
+    }
+    if (b == 0 && t == 0) p.offs[0] = 0ull;
+    __syncthreads();
+    // pass 2: per thread 8 consecutive counts; one block-wide scan per chunk
+    uint32_t carryV = sPrefix[0], carryT = sPrefix[1];
+    for (uint32_t c = 0; c < p.scanChunks; ++c) {
+        const uint32_t e0 = lo + c * kScanItems + (uint32_t)t * 8u;
+        if (c > 0) {
+            ch.load(p.counts, e0, hi);
+            ch.sum(sv, st);
+            __syncthreads();  // sWave reuse
+        }
+        const uint32_t iv = wave_incl_scan(sv), it = wave_incl_scan(st);
+        if (lane == 63) {
+            sWave[0][wv] = iv;
+            sWave[1][wv] = it;
+        }
+        __syncthreads();
+        uint32_t runV = carryV + iv - sv, runT = carryT + it - st;
+        uint32_t totV = 0u, totT = 0u;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            const uint32_t a = sWave[0][w], bb = sWave[1][w];
+            runV += w < wv ? a : 0u;
+            runT += w < wv ? bb : 0u;
+            totV += a;
+            totT += bb;
+        }
+        uint64_t out[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            runV += (uint32_t)ch.c[i];
+            runT += (uint32_t)(ch.c[i] >> 32);
+            out[i] = (uint64_t)runV | ((uint64_t)runT << 32);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (e0 + i < hi) p.offs[e0 + i + 1] = out[i];
+        carryV += totV;
+        carryT += totT;
+    }
+}
+
 // Vertices: batches of 16 vertices per wavefront iteration, one quad per vertex.
 // Phase A (quad pruning): the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762)
 // Phase B (per-lane pruning): lane 0 = p with colour, lanes 1..3 = p + delta*e_a
@@ -764,6 +922,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const float r = (float)j * third;
     const float delta = 0.001f;
     const float inv = -1.0f / delta;
+    if (blockIdx.x < p.scanBlocks) scan_counts_block(p, blockIdx.x);  // block-uniform
     const ShardBatches sb(&p.ctr->shard[0].v, p.vShardCap, 16);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
@@ -774,8 +933,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         if (!valid) rec = first;
         rec += shard * p.vShardCap;
         const VertexRec R = p.vq[rec];
-        const uint32_t outBase = (uint32_t)p.offs[R.w];  // consumed at the end: latency overlaps the walk
-        const uint32_t m = R.m;
+        const uint32_t m = p.mpuBegin + R.w;
         float o[3];
         mpu_origin(p, m, o);
         const uint32_t key = R.vidKey >> 16;
@@ -834,10 +992,10 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         nx = nx * im;
         ny = ny * im;
         nz = nz * im;
-        const uint32_t gi = outBase + (R.vidKey & 0xffffu);
-        if (valid && j == 0 && gi < p.vCap) {  // past vCap: finish() grows and re-runs
-            p.pos[gi * 3 + 0] = P0; p.pos[gi * 3 + 1] = P1; p.pos[gi * 3 + 2] = P2;
-            p.nrm[gi * 3 + 0] = nx; p.nrm[gi * 3 + 1] = ny; p.nrm[gi * 3 + 2] = nz;
+        if (valid && j == 0) {  // into the record; k_finish places it in the mesh
+            VertexRec& out = p.vq[rec];
+            out.pos[0] = P0; out.pos[1] = P1; out.pos[2] = P2;
+            out.nrm[0] = nx; out.nrm[1] = ny; out.nrm[2] = nz;
         }
     }
 }
@@ -851,7 +1009,6 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
-    const uint32_t nV = min((uint32_t)p.offs[p.mpuCount], p.vCap);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
     if (blockIdx.x == 0) {  // the run's counters for the host (mapped pinned memory)
@@ -859,25 +1016,38 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         uint32_t* dst = reinterpret_cast<uint32_t*>(p.hostCtr);
         for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) dst[i] = src[i];
         __threadfence_system();
-        // the next run's counters and k_scan words (no kernel of this run touches them)
+        // the next run's counters and offsets-scan words (no kernel of this run touches them)
         uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
         for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
         for (uint32_t i = threadIdx.x; i < kScanMaxBlocks; i += blockDim.x) p.scanStatusNext[i] = 0ull;
     }
-    for (uint32_t b = wave0; b * 64 < nV; b += nWaves) {
-        uint32_t g = b * 64 + lane;
-        const bool valid = g < nV;
-        if (!valid) g = b * 64;
-        const float x = p.pos[g * 3 + 0], y = p.pos[g * 3 + 1], z = p.pos[g * 3 + 2];
-        const CullMask cm = cull_mask_points(M, x, y, z, p.cull != 0);
-        float c[3];
-        (void)ev.template eval<1, true>(x, y, z, cm, c);
-        if (valid) {
-            p.col[g * 3 + 0] = c[0];
-            p.col[g * 3 + 1] = c[1];
-            p.col[g * 3 + 2] = c[2];
+    const ShardBatches sv(&p.ctr->shard[0].v, p.vShardCap, 64);
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sv.locate(batch, &shard, &first, &count);
+        uint32_t rec = first + (uint32_t)lane;
+        const bool valid = rec < count;
+        if (!valid) rec = first;
+        const VertexRec R = p.vq[(size_t)shard * p.vShardCap + rec];
+        const uint32_t gi = (uint32_t)p.offs[R.w] + (R.vidKey & 0xffffu);
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        if (!(p.debug & 32u)) {  // ablation bit 5: no colour walk
+            const CullMask cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], p.cull != 0);
+            (void)ev.template eval<1, true>(R.pos[0], R.pos[1], R.pos[2], cm, c);
+        }
+        if (valid && gi < p.vCap) {  // past vCap: finish() grows and re-runs
+            p.pos[gi * 3 + 0] = R.pos[0];
+            p.pos[gi * 3 + 1] = R.pos[1];
+            p.pos[gi * 3 + 2] = R.pos[2];
+            p.nrm[gi * 3 + 0] = R.nrm[0];
+            p.nrm[gi * 3 + 1] = R.nrm[1];
+            p.nrm[gi * 3 + 2] = R.nrm[2];
+            p.col[gi * 3 + 0] = c[0];
+            p.col[gi * 3 + 1] = c[1];
+            p.col[gi * 3 + 2] = c[2];
         }
     }
+    if (p.debug & 64u) return;  // ablation bit 6: no triangles
     const ShardBatches sb(&p.ctr->shard[0].t, p.tShardCap, 64);
     for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;

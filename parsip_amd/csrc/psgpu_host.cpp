@@ -241,6 +241,36 @@ int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, con
         d.resY = O.resY[i];
         d.type = O.opType[i];
     }
+    // Colour of each op whose subtree is all +0 fields (culled primitives, or pruned: the
+    // reference's colour pass then reads zeroed arrays, :1472-1522): a constant of the tree
+    // and the primitive colours, computed in fp32 exactly as op_colour_weights + the
+    // weighted sum on the device.  Ops are numbered pre-order: children have larger ids.
+    for (int op = (int)O.ctOps - 1; op >= 0; --op) {
+        const uint32_t t = O.opType[op], kind = O.opChildKind[op];
+        const uint32_t L = O.opLeftChild[op], R = O.opRightChild[op];
+        float cl[3], cr[3];
+        for (int k = 0; k < 3; ++k) {
+            const float* pc[3] = {P.colorX, P.colorY, P.colorZ};
+            cl[k] = (kind & 2) ? D.zeroCol[L][k] : pc[k][L];
+            cr[k] = (kind & 1) ? D.zeroCol[R][k] : pc[k][R];
+        }
+        const float lf = 0.0f, rf = 0.0f;
+        float v = 0.0f, wl = 0.0f, wr = 0.0f;
+        bool weighted = true;
+        switch (t) {
+        case PSGPU_OP_BLEND: v = lf + rf; wl = 2.0f * (0.5f + lf) - 1.0f; wr = 2.0f * (0.5f + rf) - 1.0f; break;
+        case PSGPU_OP_UNION: v = lf > rf ? lf : rf; wl = (v - lf) == 0.0f ? 1.0f : 0.0f; wr = (v - rf) == 0.0f ? 1.0f : 0.0f; break;
+        case PSGPU_OP_INTERSECT: v = lf < rf ? lf : rf; wl = (v - lf) == 0.0f ? 1.0f : 0.0f; wr = (v - rf) == 0.0f ? 1.0f : 0.0f; break;
+        case PSGPU_OP_DIF: { const float q = 1.0f - rf; v = lf < q ? lf : q; wl = lf == v ? 1.0f : 0.0f; wr = (1.0f - rf) == v ? 1.0f : 0.0f; } break;
+        case PSGPU_OP_SMOOTHDIF: v = lf * (1.0f - rf); wl = lf == v ? 1.0f : 0.0f; wr = (1.0f - rf) == v ? 1.0f : 0.0f; break;
+        default: weighted = false; break;
+        }
+        for (int k = 0; k < 3; ++k) {
+            if (weighted) D.zeroCol[op][k] = wl * cl[k] + wr * cr[k];
+            else if (t >= PSGPU_OP_WARPTWIST && t <= PSGPU_OP_WARPSHEAR) D.zeroCol[op][k] = cl[k];
+            else D.zeroCol[op][k] = 0.0f;  // not used: zero subtrees contain only the types above
+        }
+    }
     // every one of the 128 prim slots is uploaded: the reference evaluates whatever
     // index an op names, even past ctPrims (SOABlobPrims keeps all 128 entries)
     for (uint32_t i = 0; i < 128; ++i) {
@@ -321,8 +351,8 @@ hipError_t grow(T*& ptr, size_t& cap, size_t need) {
     return e;
 }
 
-constexpr int kNumKernels = 5;
-const char* kKernelNames[kNumKernels] = {"k_precheck", "k_mpu", "k_scan", "k_vertex", "k_finish"};
+constexpr int kNumKernels = 4;
+const char* kKernelNames[kNumKernels] = {"k_precheck", "k_mpu", "k_vertex", "k_finish"};
 
 }  // namespace
 
@@ -491,14 +521,14 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(J->mpu, kShards * ((p.pShardCap + 3) / 4), 256, mpu_lds_bytes(0), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
-    PSGPU_CHECK(launch_scan(p, s));
+    // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
+    const uint32_t gridV = std::max(persistV, p.scanBlocks);
+    if (J) PSGPU_CHECK(launch_jit(J->vertex, gridV, 256, 0, s, p));
+    else PSGPU_CHECK(launch_vertex(p, s, gridV));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-    if (J) PSGPU_CHECK(launch_jit(J->vertex, persistV, 256, 0, s, p));
-    else PSGPU_CHECK(launch_vertex(p, s, persistV));
-    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
     if (J) PSGPU_CHECK(launch_jit(J->finish, persistF, 256, 0, s, p));
     else PSGPU_CHECK(launch_finish(p, s, persistF));
-    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[5], s));
+    if (timed) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
     return PSGPU_RET_SUCCESS;
 }
 

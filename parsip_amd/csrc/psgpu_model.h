@@ -127,14 +127,15 @@ struct DevModel {
     DevOp ops[128];
     DevPrim prims[128];
     CullSeg cull[128];
+    float zeroCol[128][4];  // colour of op i when every field below it is +0 (see host)
 };
 
 // Compact-mesh work records written by the MPU kernel.
-struct VertexRec {       // 16 B: MPU slot in the range, global MPU id, local vertex id, edge key
-    uint32_t w;
-    uint32_t m;
+struct VertexRec {       // 32 B: MPU slot in the range, vid | edge key << 16, then k_vertex's
+    uint32_t w;          // position and normal (k_finish places it in the compact mesh)
     uint32_t vidKey;     // vid | key << 16, key = sx | sy<<3 | sz<<6 | axis<<9
-    uint32_t pad;
+    float pos[3];
+    float nrm[3];
 };
 struct TriRec {          // 16 B
     uint32_t w;
@@ -148,7 +149,7 @@ struct TriRec {          // 16 B
 // takes one returning atomic per MPU (a single word saturates at about 88 atomics/us
 // on MI355X: MI355X_MICROARCH.md 'dequeue').
 constexpr int kShards = 64;
-constexpr uint32_t kScanItems = 8192;   // k_scan: counts per block per chunk (1024 x 8)
+constexpr uint32_t kScanItems = 2048;   // offsets scan: counts per 256-thread block per chunk
 constexpr uint32_t kScanMaxBlocks = 256;
 struct ShardCtr {           // one 128-B line per shard: atomics on one line serialise
     uint32_t p;             // S1 survivors appended
@@ -159,7 +160,7 @@ struct ShardCtr {           // one 128-B line per shard: atomics on one line ser
 };
 struct DevCounters {
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
-    uint32_t error;          // protocol errors (bit 0: k_scan look-back timeout)
+    uint32_t error;          // protocol errors (bit 0: offsets-scan look-back timeout)
     uint32_t pad[30];
     ShardCtr shard[kShards];
 };
@@ -182,10 +183,10 @@ struct Params {
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
     uint64_t* offs;         // mpuCount + 1: exclusive scan of counts
-    uint64_t* scanStatus;   // k_scan look-back words of this run (zeroed by the previous run)
+    uint64_t* scanStatus;   // offsets-scan look-back words of this run (zeroed by the previous run)
     uint64_t* scanStatusNext;
-    uint32_t scanBlocks;    // k_scan blocks
-    uint32_t scanChunks;    // kScanItems chunks per k_scan block
+    uint32_t scanBlocks;    // offsets-scan blocks (the first blocks of k_vertex)
+    uint32_t scanChunks;    // kScanItems chunks per scan block
     VertexRec* vq;          // kShards queues of vShardCap records
     uint32_t vShardCap;
     TriRec* tq;             // kShards queues of tShardCap records
