@@ -519,7 +519,8 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
 }
 
 #ifndef PSGPU_S2_N
-#define PSGPU_S2_N 1  // x-slices per walk in S2 (1, 2, 4 or 8)
+#define PSGPU_S2_N 8  // x-slices per walk in S2 (1, 2, 4 or 8): one walk per (y,z) needle
+                      // shares each primitive's uniform work and (y,z) terms over 8 points
 #endif
 constexpr int kLdsFv = 0;
 constexpr int kLdsEdge = 0;  // edgeVid reuses the field cache: fv is dead after pass 1
