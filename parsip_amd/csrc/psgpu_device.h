@@ -908,12 +908,40 @@ __device__ __forceinline__ void scan_counts_block(const Params& p, uint32_t b) {
     }
 }
 
-// Vertices: batches of 16 vertices per wavefront iteration, one quad per vertex.
+// Cull mask for the AABB of N points per lane (all 64 lanes must participate),
+// grown by `ext` on the high side of every axis.
+template <int N>
+__device__ __forceinline__ CullMask cull_mask_points_n(ModelPtr M, const float* px, const float* py, const float* pz,
+                                                       bool enable, float ext = 0.0f) {
+    if (!enable) return CullMask{0ull, 0ull};
+    bool nan = false;
+    float x0 = px[0], x1 = px[0], y0 = py[0], y1 = py[0], z0 = pz[0], z1 = pz[0];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        nan = nan || !(px[n] == px[n]) || !(py[n] == py[n]) || !(pz[n] == pz[n]);
+        x0 = fminf(x0, px[n]); x1 = fmaxf(x1, px[n]);
+        y0 = fminf(y0, py[n]); y1 = fmaxf(y1, py[n]);
+        z0 = fminf(z0, pz[n]); z1 = fmaxf(z1, pz[n]);
+    }
+    // a NaN coordinate (fminf/fmaxf would hide it) disables culling for the wave
+    if (ballot(nan) != 0ull) return CullMask{0ull, 0ull};
+    return cull_mask_box(M, wave_min(x0), wave_min(y0), wave_min(z0), wave_max(x1) + ext, wave_max(y1) + ext,
+                         wave_max(z1) + ext);
+}
+
+#ifndef PSGPU_V_N
+#define PSGPU_V_N 1  // vertices per quad of lanes per k_vertex pass (2: bigger culling boxes, slower)
+#endif
+
+// Vertices: 16 * VN per wavefront pass, one quad of lanes per vertex and VN vertices
+// per quad (vertex first + quad + 16n), each walk evaluating VN points per lane.
 // Phase A (quad pruning): the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762)
-// Phase B (per-lane pruning): lane 0 = p with colour, lanes 1..3 = p + delta*e_a
-// (fieldValueAndColor + normal, :764-807).
+// Phase B (per-lane pruning): lane 0 = p, lanes 1..3 = p + delta*e_a
+// (fieldValueAndColor's value + normal, :764-807; the colour walk runs in k_finish).
+// Position and normal go into the vertex record; k_finish places them in the mesh.
 template <class EV>
 __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
+    constexpr int VN = PSGPU_V_N;
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
@@ -923,80 +951,112 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const float r = (float)j * third;
     const float delta = 0.001f;
     const float inv = -1.0f / delta;
+    const float cs = p.cs;
     if (blockIdx.x < p.scanBlocks) scan_counts_block(p, blockIdx.x);  // block-uniform
-    const ShardBatches sb(&p.ctr->shard[0].v, p.vShardCap, 16);
+    const ShardBatches sb(&p.ctr->shard[0].v, p.vShardCap, 16 * VN);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
         sb.locate(batch, &shard, &first, &count);
-        uint32_t rec = first + (lane >> 2);
-        const bool valid = rec < count;
-        if (!valid) rec = first;
-        rec += shard * p.vShardCap;
-        const VertexRec R = p.vq[rec];
-        const uint32_t m = p.mpuBegin + R.w;
-        float o[3];
-        mpu_origin(p, m, o);
-        const uint32_t key = R.vidKey >> 16;
-        const int sx = key & 7, sy = (key >> 3) & 7, sz = (key >> 6) & 7, ax = (key >> 9) & 3;
-        const float cs = p.cs;
-        // e1 = lo + cs*s, e2 = e1 with e2[axis] += cs (:722-724)
-        float e1[3] = {o[0] + cs * (float)sx, o[1] + cs * (float)sy, o[2] + cs * (float)sz};
-        float e2[3] = {e1[0], e1[1], e1[2]};
-        e2[ax] = e1[ax] + cs;
-        const float dX = e2[0] - e1[0], dY = e2[1] - e1[1], dZ = e2[2] - e1[2];
-        const float qx = e1[0] + dX * r, qy = e1[1] + dY * r, qz = e1[2] + dZ * r;
+        bool valid[VN];
+        size_t rec[VN];
+        float e1x[VN], e1y[VN], e1z[VN], dX[VN], dY[VN], dZ[VN], qx[VN], qy[VN], qz[VN];
+        uint32_t key[VN];
+#pragma unroll
+        for (int n = 0; n < VN; ++n) {
+            uint32_t rr = first + ((uint32_t)lane >> 2) + 16u * (uint32_t)n;
+            valid[n] = rr < count;
+            if (!valid[n]) rr = first;
+            rec[n] = (size_t)shard * p.vShardCap + rr;
+            const VertexRec R = p.vq[rec[n]];
+            float o[3];
+            mpu_origin(p, p.mpuBegin + R.w, o);
+            key[n] = R.vidKey >> 16;
+            const int sx = key[n] & 7, sy = (key[n] >> 3) & 7, sz = (key[n] >> 6) & 7, ax = (key[n] >> 9) & 3;
+            // e1 = lo + cs*s, e2 = e1 with e2[axis] += cs (:722-724)
+            e1x[n] = o[0] + cs * (float)sx;
+            e1y[n] = o[1] + cs * (float)sy;
+            e1z[n] = o[2] + cs * (float)sz;
+            const float e2x = ax == 0 ? e1x[n] + cs : e1x[n];
+            const float e2y = ax == 1 ? e1y[n] + cs : e1y[n];
+            const float e2z = ax == 2 ? e1z[n] + cs : e1z[n];
+            dX[n] = e2x - e1x[n];
+            dY[n] = e2y - e1y[n];
+            dZ[n] = e2z - e1z[n];
+            qx[n] = e1x[n] + dX[n] * r;
+            qy[n] = e1y[n] + dY[n] * r;
+            qz[n] = e1z[n] + dZ[n] * r;
+        }
         // the edge samples' AABB grown by delta also covers p + delta*e_a whenever p lies on
         // the bracketing segment (0 <= scale <= 1); phase B recomputes the mask otherwise
-        const CullMask cm = cull_mask_points(M, qx, qy, qz, p.cull != 0, delta);
-        const float f = ev.template eval<4, false>(qx, qy, qz, cm, nullptr);
-        float fs[4], xs[4], ys[4], zs[4];
-        fs[0] = quad_bcast<0>(f);
-        fs[1] = quad_bcast<1>(f);
-        fs[2] = quad_bcast<2>(f);
-        fs[3] = quad_bcast<3>(f);
+        const CullMask cm = cull_mask_points_n<VN>(M, qx, qy, qz, p.cull != 0, delta);
+        float f[VN];
+        if (p.debug & 256u) {  // ablation bit 8: no phase-A walk
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const float rs = (float)s * third;
-            xs[s] = e1[0] + dX * rs;
-            ys[s] = e1[1] + dY * rs;
-            zs[s] = e1[2] + dZ * rs;
+            for (int n = 0; n < VN; ++n) f[n] = qx[n];
+        } else {
+            ev.template evaln<4, false, VN>(qx, qy, qz, cm, f, nullptr);
         }
-        // first sample whose inside state differs from sample 0, else 3 (:744-755)
-        const bool st0 = fs[0] >= 0.5f;
-        const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
-        const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
-        const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
-        const float ax0 = iv == 1 ? xs[0] : (iv == 2 ? xs[1] : xs[2]);
-        const float ay0 = iv == 1 ? ys[0] : (iv == 2 ? ys[1] : ys[2]);
-        const float az0 = iv == 1 ? zs[0] : (iv == 2 ? zs[1] : zs[2]);
-        const float bx0 = iv == 1 ? xs[1] : (iv == 2 ? xs[2] : xs[3]);
-        const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
-        const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
-        const float scale = (0.5f - fa) / (fb - fa);
-        const float P0 = ax0 + scale * (bx0 - ax0);
-        const float P1 = ay0 + scale * (by0 - ay0);
-        const float P2 = az0 + scale * (bz0 - az0);
-        const float qx2 = j == 1 ? P0 + delta : P0;
-        const float qy2 = j == 2 ? P1 + delta : P1;
-        const float qz2 = j == 3 ? P2 + delta : P2;
-        // fieldValue at p and at the three normal samples; the colour walk at p runs in
-        // finish_body, 64 vertices per wave (colour work is needed at 1 point in 4)
-        // p off its edge (no sign change in the samples, or inf/NaN): box of the actual points
-        const bool onEdge = scale >= 0.0f && scale <= 1.0f;
-        const CullMask cmB = ballot(!onEdge) == 0ull ? cm : cull_mask_points(M, qx2, qy2, qz2, p.cull != 0);
-        const float g = ev.template eval<1, false>(qx2, qy2, qz2, cmB, nullptr);
-        const float vtx = quad_bcast<0>(g);
-        const float gx = quad_bcast<1>(g), gy = quad_bcast<2>(g), gz = quad_bcast<3>(g);
-        float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
-        const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);  // SimdNormalize
-        nx = nx * im;
-        ny = ny * im;
-        nz = nz * im;
-        if (valid && j == 0) {  // into the record; k_finish places it in the mesh
-            VertexRec& out = p.vq[rec];
-            out.pos[0] = P0; out.pos[1] = P1; out.pos[2] = P2;
-            out.nrm[0] = nx; out.nrm[1] = ny; out.nrm[2] = nz;
+        float P0[VN], P1[VN], P2[VN], qx2[VN], qy2[VN], qz2[VN];
+        bool offEdge = false;
+#pragma unroll
+        for (int n = 0; n < VN; ++n) {
+            float fs[4], xs[4], ys[4], zs[4];
+            fs[0] = quad_bcast<0>(f[n]);
+            fs[1] = quad_bcast<1>(f[n]);
+            fs[2] = quad_bcast<2>(f[n]);
+            fs[3] = quad_bcast<3>(f[n]);
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const float rs = (float)s2 * third;
+                xs[s2] = e1x[n] + dX[n] * rs;
+                ys[s2] = e1y[n] + dY[n] * rs;
+                zs[s2] = e1z[n] + dZ[n] * rs;
+            }
+            // first sample whose inside state differs from sample 0, else 3 (:744-755)
+            const bool st0 = fs[0] >= 0.5f;
+            const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
+            const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
+            const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
+            const float ax0 = iv == 1 ? xs[0] : (iv == 2 ? xs[1] : xs[2]);
+            const float ay0 = iv == 1 ? ys[0] : (iv == 2 ? ys[1] : ys[2]);
+            const float az0 = iv == 1 ? zs[0] : (iv == 2 ? zs[1] : zs[2]);
+            const float bx0 = iv == 1 ? xs[1] : (iv == 2 ? xs[2] : xs[3]);
+            const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
+            const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
+            const float scale = (0.5f - fa) / (fb - fa);
+            P0[n] = ax0 + scale * (bx0 - ax0);
+            P1[n] = ay0 + scale * (by0 - ay0);
+            P2[n] = az0 + scale * (bz0 - az0);
+            qx2[n] = j == 1 ? P0[n] + delta : P0[n];
+            qy2[n] = j == 2 ? P1[n] + delta : P1[n];
+            qz2[n] = j == 3 ? P2[n] + delta : P2[n];
+            // p off its edge (no sign change in the samples, or inf/NaN)
+            offEdge = offEdge || (valid[n] && !(scale >= 0.0f && scale <= 1.0f));
+        }
+        // fieldValue at p and at the three normal samples
+        const CullMask cmB = ballot(offEdge) == 0ull ? cm : cull_mask_points_n<VN>(M, qx2, qy2, qz2, p.cull != 0);
+        float g[VN];
+        if (p.debug & 128u) {  // ablation bit 7: no phase-B walk
+#pragma unroll
+            for (int n = 0; n < VN; ++n) g[n] = f[n];
+        } else {
+            ev.template evaln<1, false, VN>(qx2, qy2, qz2, cmB, g, nullptr);
+        }
+#pragma unroll
+        for (int n = 0; n < VN; ++n) {
+            const float vtx = quad_bcast<0>(g[n]);
+            const float gx = quad_bcast<1>(g[n]), gy = quad_bcast<2>(g[n]), gz = quad_bcast<3>(g[n]);
+            float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
+            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);  // SimdNormalize
+            nx = nx * im;
+            ny = ny * im;
+            nz = nz * im;
+            if (valid[n] && j == 0) {  // into the record; k_finish places it in the mesh
+                VertexRec& out = p.vq[rec[n]];
+                out.pos[0] = P0[n]; out.pos[1] = P1[n]; out.pos[2] = P2[n];
+                out.nrm[0] = nx; out.nrm[1] = ny; out.nrm[2] = nz;
+            }
         }
     }
 }
