@@ -665,6 +665,14 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     }
     qv = lane_value(qv, 0);
     qt = lane_value(qt, 0);
+    if (p.cull && V > 0u) {  // culling mask of the MPU box grown by the normal delta, for k_vertex
+        const float e = 7.0f * cs + 0.001f;
+        const CullMask cg = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
+        if (lane == 0) {
+            p.mpuMasks[2 * w] = cg.lo;
+            p.mpuMasks[2 * w + 1] = cg.hi;
+        }
+    }
     VertexRec* vq = p.vq + (size_t)shard * p.vShardCap;
     TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -697,9 +705,12 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
             edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
             const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
             const uint32_t g = qv + r;
-            if (g < p.vShardCap) {
+            if (g < p.vShardCap) {  // pos holds the MPU origin until k_vertex writes the vertex
                 vq[g].w = w;
                 vq[g].vidKey = r | (key << 16);
+                vq[g].pos[0] = o[0];
+                vq[g].pos[1] = o[1];
+                vq[g].pos[2] = o[2];
             }
         }
     }
@@ -961,7 +972,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         bool valid[VN];
         size_t rec[VN];
         float e1x[VN], e1y[VN], e1z[VN], dX[VN], dY[VN], dZ[VN], qx[VN], qy[VN], qz[VN];
-        uint32_t key[VN];
+        uint32_t key[VN], wrec[VN];
 #pragma unroll
         for (int n = 0; n < VN; ++n) {
             uint32_t rr = first + ((uint32_t)lane >> 2) + 16u * (uint32_t)n;
@@ -969,8 +980,8 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             if (!valid[n]) rr = first;
             rec[n] = (size_t)shard * p.vShardCap + rr;
             const VertexRec R = p.vq[rec[n]];
-            float o[3];
-            mpu_origin(p, p.mpuBegin + R.w, o);
+            const float o[3] = {R.pos[0], R.pos[1], R.pos[2]};  // the MPU origin (k_mpu)
+            wrec[n] = R.w;
             key[n] = R.vidKey >> 16;
             const int sx = key[n] & 7, sy = (key[n] >> 3) & 7, sz = (key[n] >> 6) & 7, ax = (key[n] >> 9) & 3;
             // e1 = lo + cs*s, e2 = e1 with e2[axis] += cs (:722-724)
@@ -989,7 +1000,19 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         }
         // the edge samples' AABB grown by delta also covers p + delta*e_a whenever p lies on
         // the bracketing segment (0 <= scale <= 1); phase B recomputes the mask otherwise
-        const CullMask cm = cull_mask_points_n<VN>(M, qx, qy, qz, p.cull != 0, delta);
+        // one MPU in the whole pass: its box grown by delta (k_mpu's mask) covers every sample
+        // and, while the roots stay on their segments, every normal sample
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(wrec[0]);
+        bool oneMpu = true;
+#pragma unroll
+        for (int n = 0; n < VN; ++n) oneMpu = oneMpu && wrec[n] == w0;
+        CullMask cm;
+        if (p.cull && ballot(!oneMpu) == 0ull) {
+            cm.lo = p.mpuMasks[2 * w0];
+            cm.hi = p.mpuMasks[2 * w0 + 1];
+        } else {
+            cm = cull_mask_points_n<VN>(M, qx, qy, qz, p.cull != 0, delta);
+        }
         float f[VN];
         if (p.debug & 256u) {  // ablation bit 8: no phase-A walk
 #pragma unroll

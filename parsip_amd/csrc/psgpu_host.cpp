@@ -387,6 +387,8 @@ struct psgpu_ctx {
     uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
     uint32_t parity = 0;            // which counter / status set the next run uses
     uint64_t* counts = nullptr;
+    uint64_t* mpuMasks = nullptr;
+    size_t capMasks = 0;
     uint64_t* offs = nullptr;
     VertexRec* vq = nullptr;
     TriRec* tq = nullptr;
@@ -447,6 +449,7 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
     PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
+    PSGPU_CHECK(grow(c->mpuMasks, c->capMasks, 2 * n));
     PSGPU_CHECK(grow(c->offs, c->capOff, n + 1));
     PSGPU_CHECK(grow(c->vq, c->capVq, (size_t)c->vShardCap * kShards));
     PSGPU_CHECK(grow(c->tq, c->capTq, (size_t)c->tShardCap * kShards));
@@ -482,6 +485,7 @@ Params make_params(psgpu_ctx* c) {
     p.scanStatus = c->scanStatus + (size_t)c->parity * kScanMaxBlocks;
     p.scanStatusNext = c->scanStatus + (size_t)(c->parity ^ 1u) * kScanMaxBlocks;
     p.counts = c->counts;
+    p.mpuMasks = c->mpuMasks;
     p.offs = c->offs;
     p.vq = c->vq;
     p.vShardCap = c->vShardCap;
@@ -791,7 +795,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graphs(c);
     c->jit.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->offs, c->vq, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->mpuMasks, c->offs, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr};
     for (void* b : bufs)
         if (b) (void)hipFree(b);

@@ -182,6 +182,7 @@ struct Params {
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
+    uint64_t* mpuMasks;     // 2 * mpuCount: culling mask of each surface MPU's box + delta
     uint64_t* offs;         // mpuCount + 1: exclusive scan of counts
     uint64_t* scanStatus;   // offsets-scan look-back words of this run (zeroed by the previous run)
     uint64_t* scanStatusNext;
