@@ -43,6 +43,19 @@
 
 typedef __m128 V4;
 
+/* Work counters (lane-evaluations, 4 per SIMD call) of the reference algorithm as
+ * executed, per phase: 0 S1, 1 S2, 2 S4 root samples, 3 S5 value/normal samples,
+ * 4 fieldValueAndColor.  Slots: [type] primitive evaluations by skeletType (0..15),
+ * [16] primitive matrices applied, [17] depth>3 op-box tests, [18] colour op steps,
+ * [32 + opType] op evaluations by type.  For the algorithmic-work figure of bench.py
+ * (tests/golden/make_workload_ops.py); they do not affect any result. */
+#define PSOR_NCNT 64
+static __thread int t_phase;
+static __thread uint64_t t_cnt[5][PSOR_NCNT];
+static uint64_t g_cnt[5][PSOR_NCNT];
+static pthread_mutex_t g_cnt_mu = PTHREAD_MUTEX_INITIALIZER;
+#define CNT(slot) (t_cnt[t_phase][(slot)] += 4)
+
 #define V(a) _mm_set1_ps(a)
 #define ADD _mm_add_ps
 #define SUB _mm_sub_ps
@@ -147,6 +160,8 @@ static V4 prim_field(const PsModelRef* m, uint32_t idx, V4 pX, V4 pY, V4 pZ) {
     V4 d2 = _mm_setzero_ps();
     V4 x = pX, y = pY, z = pZ;
     uint32_t im = P->idxMatrix[idx];
+    CNT(P->skeletType[idx] & 15);
+    if (im != 0) CNT(16);
     if (im != 0) { /* :948-970, rows ((m0*x + m1*y) + m2*z) + m3 */
         const float* M = &m->mats->matrix[im * PSGPU_PRIM_MATRIX_STRIDE];
         x = ADD(ADD(ADD(MUL(V(M[0]), pX), MUL(V(M[1]), pY)), MUL(V(M[2]), pZ)), V(M[3]));
@@ -254,6 +269,7 @@ static V4 field_value(const PsModelRef* m, V4 pX, V4 pY, V4 pZ, float* primF, fl
             uint32_t L = O->opLeftChild[op], R = O->opRightChild[op];
             uint32_t kind = O->opChildKind[op];
             int lop = (kind & 2) >> 1, rop = kind & 1;
+            if (depth > 3 && !computed[op]) CNT(17);
             if (depth > 3) { /* :1228-1252, OR of the three axis slabs, per 4 lanes */
                 V4 in = _mm_and_ps(_mm_cmpge_ps(pX, V(O->vBoxLoX[op])), _mm_cmpge_ps(V(O->vBoxHiX[op]), pX));
                 in = _mm_or_ps(in, _mm_and_ps(_mm_cmpge_ps(pY, V(O->vBoxLoY[op])), _mm_cmpge_ps(V(O->vBoxHiY[op]), pY)));
@@ -274,6 +290,7 @@ static V4 field_value(const PsModelRef* m, V4 pX, V4 pY, V4 pZ, float* primF, fl
                 else { lf = prim_field(m, L, pX, pY, pZ); _mm_storeu_ps(&primF[L * 4], lf); }
                 if (rop) rf = _mm_loadu_ps(&opF[R * 4]);
                 else { rf = prim_field(m, R, pX, pY, pZ); _mm_storeu_ps(&primF[R * 4], rf); }
+                CNT(32 + (O->opType[op] & 31));
                 switch (O->opType[op]) { /* :1282-1338 */
                 case PSGPU_OP_BLEND: out = ADD(lf, rf); break;
                 case PSGPU_OP_RICCIBLEND: { /* fast_pow, PS_SIMDVecN.h:122-128 */
@@ -341,6 +358,7 @@ static V4 field_and_color(const PsModelRef* m, V4 pX, V4 pY, V4 pZ, V4* cX, V4* 
             int ready = !((lop && !done[L]) || (rop && !done[R]));
             if (ready) {
                 --top;
+                CNT(18);
                 V4 cur = _mm_loadu_ps(&opF[op * 4]);
                 V4 lf, rf, lcx, lcy, lcz, rcx, rcy, rcz;
                 if (lop) { lf = _mm_loadu_ps(&opF[L * 4]); lcx = V(colX[L * 4]); lcy = V(colY[L * 4]); lcz = V(colZ[L * 4]); }
@@ -455,6 +473,7 @@ typedef struct MpuOut {
 
 static void process_mpu(const PsModelRef* m, float cs, PsVec3f lo, MpuOut* o, float* vbuf, uint16_t* tbuf) {
     memset(o, 0, sizeof(*o));
+    t_phase = 0;
     /* S1: 8 MPU corners as two quads (:483-540) */
     {
         const float side = 7.0f * cs;
@@ -467,6 +486,7 @@ static void process_mpu(const PsModelRef* m, float cs, PsVec3f lo, MpuOut* o, fl
         if (m1 == 0 && m2 == 0) return;
     }
     o->passed = 1;
+    t_phase = 1;
     /* S2: 8^3 field cache, z in quads of 4 (:550-610); fv[x][y][z] */
     float fv[8][8][8];
     int ctIn = 0, ctOut = 0;
@@ -515,6 +535,7 @@ static void process_mpu(const PsModelRef* m, float cs, PsVec3f lo, MpuOut* o, fl
                         V4 qx = ADD(V(e1[0]), MUL(V(e2[0] - e1[0]), rootRes));
                         V4 qy = ADD(V(e1[1]), MUL(V(e2[1] - e1[1]), rootRes));
                         V4 qz = ADD(V(e1[2]), MUL(V(e2[2] - e1[2]), rootRes));
+                        t_phase = 2;
                         V4 rf = field_only(m, qx, qy, qz);
                         int in = _mm_movemask_ps(_mm_cmpge_ps(rf, V(PSGPU_ISO_VALUE)));
                         int state = in & 1, iv = 0;
@@ -530,7 +551,9 @@ static void process_mpu(const PsModelRef* m, float cs, PsVec3f lo, MpuOut* o, fl
                         for (int c = 0; c < 3; ++c) p[c] = a[c] + scale * (b[c] - a[c]);
                         /* S5: field + colour + normal (:764-807) */
                         V4 cx, cy, cz, nx, ny, nz;
+                        t_phase = 4;
                         V4 vf = field_and_color(m, V(p[0]), V(p[1]), V(p[2]), &cx, &cy, &cz);
+                        t_phase = 3;
                         normal_at(m, V(p[0]), V(p[1]), V(p[2]), vf, &nx, &ny, &nz);
                         if (ctV >= PSGPU_MAX_MPU_VERTEX_COUNT * 4) { o->overflow = 1; v = 0; }
                         else {
@@ -586,6 +609,7 @@ typedef struct Job {
 
 static void* worker(void* arg) {
     Job* J = (Job*)arg;
+    memset(t_cnt, 0, sizeof(t_cnt));
     float* vbuf = (float*)malloc((size_t)PSGPU_MAX_MPU_VERTEX_COUNT * 4 * 9 * sizeof(float));
     uint16_t* tbuf = (uint16_t*)malloc((size_t)PSGPU_MAX_MPU_TRIANGLE_COUNT * 4 * 3 * sizeof(uint16_t));
     for (;;) {
@@ -605,7 +629,18 @@ static void* worker(void* arg) {
     }
     free(vbuf);
     free(tbuf);
+    pthread_mutex_lock(&g_cnt_mu);
+    for (int ph = 0; ph < 5; ++ph)
+        for (int k = 0; k < PSOR_NCNT; ++k) g_cnt[ph][k] += t_cnt[ph][k];
+    pthread_mutex_unlock(&g_cnt_mu);
     return NULL;
+}
+
+/* Work counters of the last psor_polygonize (see t_cnt). */
+void psor_work_counts(uint64_t out[5 * PSOR_NCNT]) {
+    pthread_mutex_lock(&g_cnt_mu);
+    memcpy(out, g_cnt, sizeof(g_cnt));
+    pthread_mutex_unlock(&g_cnt_mu);
 }
 
 int psor_polygonize(float cellsize, const PsModelRef* m, uint32_t mpuBegin, uint32_t mpuEnd, int nthreads,
@@ -626,6 +661,9 @@ int psor_polygonize(float cellsize, const PsModelRef* m, uint32_t mpuBegin, uint
     J.count = mpuEnd - mpuBegin;
     J.out = (MpuOut*)calloc(J.count ? J.count : 1, sizeof(MpuOut));
     J.keep = keepMesh;
+    pthread_mutex_lock(&g_cnt_mu);
+    memset(g_cnt, 0, sizeof(g_cnt));
+    pthread_mutex_unlock(&g_cnt_mu);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];

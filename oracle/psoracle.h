@@ -27,6 +27,7 @@ int psor_polygonize(float cellsize, const PsModelRef* m, uint32_t mpuBegin, uint
 void psor_result_info(const psor_result* r, uint32_t* ctMPUs, uint32_t* ctV, uint32_t* ctT);
 void psor_result_copy(const psor_result* r, uint32_t* stats5, float* pos, float* nrm, float* col, uint16_t* tri);
 void psor_result_free(psor_result* r);
+void psor_work_counts(uint64_t out[5 * 64]);
 int psor_prepare_bboxes(PsSoaBlobPrims* P, const PsSoaBoxMatrices* BM, PsSoaBlobOps* O);
 
 #ifdef __cplusplus

@@ -48,6 +48,7 @@ def lib(sse_approx: bool = False):
         L.psor_tritable.argtypes = [vp]
         L.psor_prepare_bboxes.argtypes = [vp, vp, vp]
         L.psor_prepare_bboxes.restype = ctypes.c_int
+        L.psor_work_counts.argtypes = [vp]
         _LIBS[key] = L
     return _LIBS[key]
 
@@ -151,3 +152,14 @@ def count_mpus(cellsize, lo, hi) -> int:
 
 def prepare_bboxes(model) -> int:
     return lib().psor_prepare_bboxes(model.prims.ctypes.data, model.boxmats.ctypes.data, model.ops.ctypes.data)
+
+
+PHASES = ("s1", "s2", "roots", "normals", "colour")
+
+
+def work_counts(sse_approx: bool = False) -> np.ndarray:
+    """(5 phases x 64 slots) lane-evaluation counters of the last polygonize: see the
+    t_cnt comment in psoracle.c."""
+    out = np.zeros((5, 64), np.uint64)
+    lib(sse_approx).psor_work_counts(out.ctypes.data)
+    return out

@@ -230,3 +230,19 @@ def test_count_mpus_lattice(oracle):
         n = oracle.count_mpus(cs, lo, hi)
         assert n == soa.count_mpus(cs, lo, hi)
     assert oracle.count_mpus(8 / 256, (-4, -4, -4), (4, 4, 4)) == 37 ** 3
+
+
+def test_workload_ops_fixture(oracle):
+    """tests/golden/workload_ops.json (bench.py's algorithmic-work figure) is what the
+    oracle's counters give for C2 today."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mwo", os.path.join(GOLDEN, "make_workload_ops.py"))
+    g = golden("workload_ops.json")["C2"]
+    model, cs, _ = synth.make_config("C2")
+    om = oracle.polygonize(model, cs, threads=4, keep=False)
+    c = oracle.work_counts()
+    assert int(c[1][:16].sum()) == g["prim_evals"]["s2"]
+    assert int(c[3][:16].sum()) == g["prim_evals"]["normals"]
+    assert int(om.stats[:, 2].sum()) == g["vertices"]
+    assert spec is not None
