@@ -54,7 +54,11 @@ static __thread int t_phase;
 static __thread uint64_t t_cnt[5][PSOR_NCNT];
 static uint64_t g_cnt[5][PSOR_NCNT];
 static pthread_mutex_t g_cnt_mu = PTHREAD_MUTEX_INITIALIZER;
+#ifdef PSOR_COUNT
 #define CNT(slot) (t_cnt[t_phase][(slot)] += 4)
+#else
+#define CNT(slot) ((void)0)
+#endif
 
 #define V(a) _mm_set1_ps(a)
 #define ADD _mm_add_ps

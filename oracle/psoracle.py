@@ -26,10 +26,11 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE, "CC=gcc"], check=True)
 
 
-def lib(sse_approx: bool = False):
-    key = "sse" if sse_approx else "ieee"
+def lib(sse_approx: bool = False, count: bool = False):
+    key = "count" if count else ("sse" if sse_approx else "ieee")
     if key not in _LIBS:
-        path = os.path.join(HERE, "_build", "libpsoracle_sse.so" if sse_approx else "libpsoracle.so")
+        name = "libpsoracle_count.so" if count else ("libpsoracle_sse.so" if sse_approx else "libpsoracle.so")
+        path = os.path.join(HERE, "_build", name)
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)
@@ -85,8 +86,10 @@ class OracleMesh:
 
 
 def polygonize(model, cellsize: float, mpu_begin: int = 0, mpu_end: int = 0xFFFFFFFF,
-               threads: int = 1, keep: bool = True, sse_approx: bool = False) -> OracleMesh | None:
-    L = lib(sse_approx)
+               threads: int = 1, keep: bool = True, sse_approx: bool = False,
+               count: bool = False) -> OracleMesh | None:
+    """``count=True`` runs the work-counting build (slower; see work_counts)."""
+    L = lib(sse_approx, count)
     ref = _ref(model)
     res = ctypes.c_void_p()
     rc = L.psor_polygonize(cellsize, ctypes.byref(ref), mpu_begin, mpu_end, threads, 1 if keep else 0,
@@ -157,9 +160,9 @@ def prepare_bboxes(model) -> int:
 PHASES = ("s1", "s2", "roots", "normals", "colour")
 
 
-def work_counts(sse_approx: bool = False) -> np.ndarray:
-    """(5 phases x 64 slots) lane-evaluation counters of the last polygonize: see the
-    t_cnt comment in psoracle.c."""
+def work_counts() -> np.ndarray:
+    """(5 phases x 64 slots) lane-evaluation counters of the last polygonize(count=True):
+    see the t_cnt comment in psoracle.c."""
     out = np.zeros((5, 64), np.uint64)
-    lib(sse_approx).psor_work_counts(out.ctypes.data)
+    lib(count=True).psor_work_counts(out.ctypes.data)
     return out

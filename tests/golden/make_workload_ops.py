@@ -39,7 +39,7 @@ out = {"generator": "tests/golden/make_workload_ops.py (oracle work counters x p
        "note": "fp32 operations the reference algorithm executes per polygonization, by kernel"}
 for name in ("C2", "C3", "C5"):
     model, cs, n = synth.make_config(name)
-    om = psoracle.polygonize(model, cs, threads=os.cpu_count() or 1, keep=False)
+    om = psoracle.polygonize(model, cs, threads=os.cpu_count() or 1, keep=False, count=True)
     c = psoracle.work_counts()
     ph = {p: phase_ops(c[i]) for i, p in enumerate(psoracle.PHASES)}
     prim_evals = {p: int(c[i][:16].sum()) for i, p in enumerate(psoracle.PHASES)}

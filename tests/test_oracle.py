@@ -240,7 +240,7 @@ def test_workload_ops_fixture(oracle):
     spec = importlib.util.spec_from_file_location("mwo", os.path.join(GOLDEN, "make_workload_ops.py"))
     g = golden("workload_ops.json")["C2"]
     model, cs, _ = synth.make_config("C2")
-    om = oracle.polygonize(model, cs, threads=4, keep=False)
+    om = oracle.polygonize(model, cs, threads=4, keep=False, count=True)
     c = oracle.work_counts()
     assert int(c[1][:16].sum()) == g["prim_evals"]["s2"]
     assert int(c[3][:16].sum()) == g["prim_evals"]["normals"]
