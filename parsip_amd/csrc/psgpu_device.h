@@ -97,6 +97,22 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
     return v;
 }
+// PSGPU_FOR_N(stmt): stmt once for each point n < N (N <= 8, a template parameter in
+// scope), unrolled by the preprocessor and `if constexpr` instead of a loop (the
+// generated tree walks emit thousands of these; see psgpu_jit.cpp, Gen::FN).
+#define PSGPU_N_AT(k, ...)                 \
+    if constexpr (N > k) {                 \
+        constexpr int n = k;               \
+        __VA_ARGS__                        \
+    }
+#define PSGPU_FOR_N(...)                                                                              \
+    {                                                                                                 \
+        static_assert(N >= 1 && N <= 8, "PSGPU_FOR_N: 1..8 points per lane");                         \
+        PSGPU_N_AT(0, __VA_ARGS__) PSGPU_N_AT(1, __VA_ARGS__) PSGPU_N_AT(2, __VA_ARGS__)              \
+        PSGPU_N_AT(3, __VA_ARGS__) PSGPU_N_AT(4, __VA_ARGS__) PSGPU_N_AT(5, __VA_ARGS__)              \
+        PSGPU_N_AT(6, __VA_ARGS__) PSGPU_N_AT(7, __VA_ARGS__)                                         \
+    }
+
 // Value of a wave-uniform lane (scalar read).
 __device__ __forceinline__ uint32_t lane_value(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
