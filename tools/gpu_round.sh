@@ -3,9 +3,17 @@
 # same bench command, and PMC passes (FETCH_SIZE, WRITE_SIZE, VALU mix) for the HBM traffic
 # and issue rate.  Every GPU step has its own time limit; the first failure ends the script.
 # Usage (from the repo root, on the box): bash tools/gpu_round.sh TAG
+# Only gpurun_out/ comes back from the box: afterwards, here, run
+#   bash tools/gpu_round.sh TAG --collect
+# to copy the summaries into profiles/.
 set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
+if [ "$2" = "--collect" ]; then
+  cp $OUT/kt/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv && cp $OUT/traffic.json profiles/${TAG}_traffic.json &&
+  cp $OUT/valu.json profiles/${TAG}_valu.json && cp $OUT/bench.json profiles/${TAG}_bench.json
+  exit $?
+fi
 mkdir -p $OUT profiles
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
