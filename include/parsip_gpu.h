@@ -224,6 +224,9 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        default: +4-5 us per polygonization on ROCm 7.2) */
 #define PSGPU_OPT_CAPACITY      6   /* restart output buffers at this vertex capacity (>= 64;
                                        they grow and the run repeats when exceeded) */
+#define PSGPU_OPT_BOUND        10   /* 1: k_precheck proves S1 survivors without a surface by
+                                       conservative field bounds and skips their S2 (default;
+                                       output unchanged; JIT kernels only) */
 #define PSGPU_OPT_JIT           3   /* 0 interpreter, 1 specialised per structure (default),
                                        2 specialised with parameters baked in */
 /* Host-only (no GPU): compile the model's specialised kernels with hiprtc (mode 1:

@@ -359,6 +359,117 @@ __device__ __forceinline__ bool culled(const CullMask& cm, uint32_t i) {
 }
 
 // ---------------------------------------------------------------------------
+// Field bounds over a box of lattice corners (k_precheck).  Most MPUs that pass S1 have
+// no surface: every S2 corner is inside or every one is outside, and S2 only discards
+// them (PS_Polygonizer.cpp:602-609).  An interval [lo, hi] of the field over the MPU's
+// corners decides that outcome without evaluating them: hi < 0.5 (no corner inside)
+// or lo >= 0.5 (no corner outside) gives exactly the reference result, 0 vertices and
+// 0 triangles.  The bound is conservative by construction:
+//  * each primitive's distance (Point, infinite Line, capped Cylinder, Cube: the same
+//    functions the reference evaluates, all true Euclidean distances, 1-Lipschitz) is
+//    evaluated at the box centre and widened by the half-diagonal h (+ 1e-4 and a
+//    relative 1e-4); Wyvill is monotone in the distance; the field interval is widened
+//    by kBoundEps, orders of magnitude above the fp32 rounding of either evaluation;
+//  * ops are monotone interval maps (Blend, Union, Intersect, Dif, SmoothDif, warps);
+//  * op-box pruning (depth > 3) is decided per quad of 4 z-consecutive corners: from
+//    the box's exact corner coordinates the op is pruned for every quad (field 0),
+//    for none (the op's interval), or for some (the interval joined with 0).
+// Only models whose used primitives all have finite, well-conditioned parameters, no
+// matrix, and a type above (or Triangle, field 0) are bounded (DevModel::boundable, set
+// by the host; Ricci and unknown ops are excluded), so no corner can be NaN -- except a
+// Cylinder on its own axis, where the bound gives up (ok = false) within 0.05 of it.
+constexpr float kBoundEps = 2e-4f;
+
+struct BoundBox {
+    float cx, cy, cz, h;       // centre, half-diagonal (with margin)
+    float xs[4], ys[4], zs[4]; // the box's corner coordinates per axis (z: one S2 quad)
+};
+
+template <int TYPE, class PR>
+__device__ __forceinline__ float prim_true_dist(PR& P, float x, float y, float z, float* axisD) {
+    float d2 = 0.0f;
+    if (TYPE == PSGPU_T_POINT) {
+        const float dx = x - P.pos[0], dy = y - P.pos[1], dz = z - P.pos[2];
+        d2 = dx * dx + dy * dy + dz * dz;
+    } else if (TYPE == PSGPU_T_LINE) {  // distance from the infinite line (the reference does not clamp)
+        const float ux = P.dir[0] - P.pos[0], uy = P.dir[1] - P.pos[1], uz = P.dir[2] - P.pos[2];
+        const float dx = x - P.pos[0], dy = y - P.pos[1], dz = z - P.pos[2];
+        const float t = (dx * ux + dy * uy + dz * uz) / (ux * ux + uy * uy + uz * uz);
+        const float ex = dx - t * ux, ey = dy - t * uy, ez = dz - t * uz;
+        d2 = ex * ex + ey * ey + ez * ez;
+    } else if (TYPE == PSGPU_T_CYLINDER) {  // solid cylinder: axis dir (unit), radius res0, height res1
+        const float px = x - P.pos[0], py = y - P.pos[1], pz = z - P.pos[2];
+        float yy = px * P.dir[0] + py * P.dir[1] + pz * P.dir[2];
+        const float rr = px * px + py * py + pz * pz - yy * yy;
+        const float r = __builtin_amdgcn_sqrtf(rr > 0.0f ? rr : 0.0f);
+        *axisD = r;
+        const float xx = fmaxf(r - P.res[0], 0.0f);
+        yy = yy > 0.0f ? fmaxf(yy - P.res[1], 0.0f) : yy;
+        d2 = xx * xx + yy * yy;
+    } else if (TYPE == PSGPU_T_CUBE) {
+        const float ex = fmaxf(fabsf(x - P.pos[0]) - P.res[0], 0.0f);
+        const float ey = fmaxf(fabsf(y - P.pos[1]) - P.res[0], 0.0f);
+        const float ez = fmaxf(fabsf(z - P.pos[2]) - P.res[0], 0.0f);
+        d2 = ex * ex + ey * ey + ez * ez;
+    }
+    return __builtin_amdgcn_sqrtf(d2);
+}
+
+__device__ __forceinline__ float wyvill_of_dist(float d) {
+    const float t = 1.0f - d * d;
+    return t > 0.0f ? (t * t) * t : 0.0f;
+}
+
+// Field interval of one primitive over the box (TYPE: Point, Line, Cylinder or Cube).
+template <int TYPE, class PR>
+__device__ __forceinline__ void prim_bound(PR& P, const BoundBox& B, float* lo, float* hi, bool* ok) {
+    float axisD = 1e30f;
+    const float d = prim_true_dist<TYPE, PR>(P, B.cx, B.cy, B.cz, &axisD);
+    if (TYPE == PSGPU_T_CYLINDER) *ok = *ok && (axisD - B.h > 0.05f);
+    *hi = wyvill_of_dist(fmaxf(d - B.h, 0.0f)) + kBoundEps;
+    *lo = wyvill_of_dist(d + B.h) - kBoundEps;
+}
+
+// Interval of a binary op (the monotone maps of op_field; Ricci/unknown types are not bounded).
+__device__ __forceinline__ void bound_op(uint32_t type, float ll, float lh, float rl, float rh, float* lo, float* hi) {
+    switch (type) {
+    case PSGPU_T_BLEND: *lo = ll + rl; *hi = lh + rh; break;
+    case PSGPU_T_UNION: *lo = fmaxf(ll, rl); *hi = fmaxf(lh, rh); break;
+    case PSGPU_T_INTERSECT: *lo = fminf(ll, rl); *hi = fminf(lh, rh); break;
+    case PSGPU_T_DIF: *lo = fminf(ll, 1.0f - rh); *hi = fminf(lh, 1.0f - rl); break;
+    case PSGPU_T_SMOOTHDIF: {
+        const float a = 1.0f - rh, b = 1.0f - rl;
+        const float p0 = ll * a, p1 = ll * b, p2 = lh * a, p3 = lh * b;
+        *lo = fminf(fminf(p0, p1), fminf(p2, p3));
+        *hi = fmaxf(fmaxf(p0, p1), fmaxf(p2, p3));
+    } break;
+    default: *lo = ll; *hi = lh; break;  // warps: the left child
+    }
+}
+
+// Op-box pruning of a depth > 3 op over the box's quads: a quad (x, y, 4 z) is pruned
+// iff x, y and all 4 z lie outside the op box on their axes (PS_Polygonizer.cpp:1239-1243).
+template <class OR>
+__device__ __forceinline__ void bound_prune(OR& b, const BoundBox& B, float* lo, float* hi) {
+    bool anyZ = false, allX = true, noX = true, allY = true, noY = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        anyZ = anyZ | ((B.zs[i] >= b.lo[2]) & (b.hi[2] >= B.zs[i]));
+        const bool ix = (B.xs[i] >= b.lo[0]) & (b.hi[0] >= B.xs[i]);
+        const bool iy = (B.ys[i] >= b.lo[1]) & (b.hi[1] >= B.ys[i]);
+        allX = allX & ix; noX = noX & !ix;
+        allY = allY & iy; noY = noY & !iy;
+    }
+    if (!anyZ && noX && noY) {  // every quad pruned: field exactly 0
+        *lo = 0.0f;
+        *hi = 0.0f;
+    } else if (!(anyZ || allX || allY)) {  // some quads pruned
+        *lo = fminf(*lo, 0.0f);
+        *hi = fmaxf(*hi, 0.0f);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Interpreter evaluator: the flattened walk program of psgpu_model.h.
 //   GROUP 4: pruning decided per 4-lane group (S1/S2 quads, S4 edge samples)
 //   GROUP 1: per lane (S5: the reference evaluates 4 identical lanes)
@@ -465,6 +576,13 @@ struct InterpEval {
         for (int n = 0; n < N; ++n)
             out[n] = eval<GROUP, COLOR>(px[n], py[n], pz[n], cm, COLOR ? colOut + 3 * n : nullptr);
     }
+
+    // field bounds are generated per tree (psgpu_jit.cpp); the interpreter never proves
+    __device__ __forceinline__ void bound(const BoundBox&, const CullMask&, float* lo, float* hi, bool* ok) const {
+        *lo = 0.0f;
+        *hi = 0.0f;
+        *ok = false;
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -510,28 +628,63 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const float py = Y * p.side + o[1];
     const float pz = Z * p.side + o[2];
     float f = -1.0f;
+    CullMask cm{0ull, 0ull};
     if (!(p.debug & 8u)) {  // ablation bit 3: S1 without the walk (nothing passes)
-        const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+        cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
         f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
     } else if (p.debug & 16u) {  // bit 4: the culling mask only
-        const CullMask cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+        cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
         f = (float)(cm.lo & 1ull) - 1.0f;
     }
     const uint64_t bal = ballot(valid && f > 0.0f);
     uint32_t flags8 = 0;  // bit g: MPU of lanes 8g..8g+7 passed
 #pragma unroll
     for (int q = 0; q < 8; ++q) flags8 |= (((bal >> (8 * q)) & 0xffull) != 0ull ? 1u : 0u) << q;
+    // Survivors proven empty by field bounds (see prim_bound): lane c of an MPU bounds
+    // the 4x4x4 corners [4X, 4X+3] x [4Y, 4Y+3] x [4Z, 4Z+3] of its S2 cache (its z range
+    // is exactly one S2 quad); the wave's culling box covers every MPU of the brick.
+    uint32_t proven8 = 0;
+    if (p.bound && flags8 != 0u) {
+        BoundBox B;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // the S2 coordinates (mpu_body): o + (float)index * cs
+            B.xs[i] = o[0] + (float)(4 * (c & 1) + i) * p.cs;
+            B.ys[i] = o[1] + (float)(4 * ((c >> 1) & 1) + i) * p.cs;
+            B.zs[i] = o[2] + (float)(4 * (c >> 2) + i) * p.cs;
+        }
+        const float hx = 0.5f * (B.xs[3] - B.xs[0]), hy = 0.5f * (B.ys[3] - B.ys[0]), hz = 0.5f * (B.zs[3] - B.zs[0]);
+        B.cx = 0.5f * (B.xs[0] + B.xs[3]);
+        B.cy = 0.5f * (B.ys[0] + B.ys[3]);
+        B.cz = 0.5f * (B.zs[0] + B.zs[3]);
+        B.h = __builtin_amdgcn_sqrtf(hx * hx + hy * hy + hz * hz) * 1.0001f + 1e-4f;
+        float lo = 0.0f, hi = 0.0f;
+        bool ok = true;
+        ev.bound(B, cm, &lo, &hi, &ok);
+        const uint64_t bOut = ballot(ok && hi < 0.5f), bIn = ballot(ok && lo >= 0.5f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bool all = ((bOut >> (8 * q)) & 0xffull) == 0xffull || ((bIn >> (8 * q)) & 0xffull) == 0xffull;
+            proven8 |= (all ? 1u : 0u) << q;
+        }
+        proven8 &= flags8;
+    }
+    const uint32_t queue8 = flags8 & ~proven8;
     // lane g < 8 speaks for MPU g (its values are those of lane 8g)
     const uint32_t mOf = __shfl(m, lane * 8 & 63);
     const bool vOf = __shfl(valid ? 1 : 0, lane * 8 & 63) != 0;
-    const bool pass = lane < 8 && ((flags8 >> lane) & 1u);
-    if (lane < 8 && vOf && !pass) p.counts[mOf - p.mpuBegin] = 0ull;
+    const bool pass = lane < 8 && ((queue8 >> lane) & 1u);
+    if (lane < 8 && vOf) {
+        p.passed[mOf - p.mpuBegin] = (uint8_t)((flags8 >> lane) & 1u);
+        if (!pass) p.counts[mOf - p.mpuBegin] = 0ull;
+    }
     if (flags8 == 0u) return;
     const uint32_t shard = W / (p.pShardCap / 8u);
+    if (lane == 1 && proven8 != 0u) atomicAdd(&p.ctr->shard[shard].b, (uint32_t)__popc(proven8));
+    if (queue8 == 0u) return;
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(flags8));
+    if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(queue8));
     base = lane_value(base, 0);
-    if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(flags8 & ((1u << lane) - 1u))] = mOf;
+    if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u))] = mOf;
 }
 
 #ifndef PSGPU_S2_N

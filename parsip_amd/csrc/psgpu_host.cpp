@@ -326,6 +326,19 @@ int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, con
         }
         d.cullable = flags;
     }
+    // field bounds (k_precheck, prim_bound in psgpu_device.h) need every primitive the
+    // walk evaluates to have a true-distance bound with sane parameters (the culling
+    // eligibility above) or be a Triangle (field 0), and every op a monotone map
+    bool bnd = D.nInstr > 0;
+    for (uint32_t k = 0; k < D.nInstr; ++k) {
+        const Instr& I = D.instr[k];
+        if (I.kind == kOp && !((I.type >= 14 && I.type <= 18) || (I.type >= 22 && I.type <= 25))) bnd = false;
+        if (I.kind == kPrim || I.kind == kSumPrim) {
+            const DevPrim& q = D.prims[I.idx];
+            if (!(q.type == PSGPU_PRIM_TRIANGLE || (q.cullable & 1u))) bnd = false;
+        }
+    }
+    D.boundable = bnd ? 1u : 0u;
     return PSGPU_RET_SUCCESS;
 }
 
@@ -387,6 +400,9 @@ struct psgpu_ctx {
     uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
     uint32_t parity = 0;            // which counter / status set the next run uses
     uint64_t* counts = nullptr;
+    uint8_t* passed = nullptr;      // per MPU: passed S1
+    size_t capPassed = 0;
+    int bound = 1;                  // prove S1 survivors empty by field bounds in k_precheck
     uint64_t* mpuMasks = nullptr;
     size_t capMasks = 0;
     uint64_t* offs = nullptr;
@@ -449,6 +465,7 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
     PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
+    PSGPU_CHECK(grow(c->passed, c->capPassed, n));
     PSGPU_CHECK(grow(c->mpuMasks, c->capMasks, 2 * n));
     PSGPU_CHECK(grow(c->offs, c->capOff, n + 1));
     PSGPU_CHECK(grow(c->vq, c->capVq, (size_t)c->vShardCap * kShards));
@@ -485,6 +502,8 @@ Params make_params(psgpu_ctx* c) {
     p.scanStatus = c->scanStatus + (size_t)c->parity * kScanMaxBlocks;
     p.scanStatusNext = c->scanStatus + (size_t)(c->parity ^ 1u) * kScanMaxBlocks;
     p.counts = c->counts;
+    p.passed = c->passed;
+    p.bound = (c->bound && c->jit && c->model.boundable) ? 1u : 0u;
     p.mpuMasks = c->mpuMasks;
     p.offs = c->offs;
     p.vq = c->vq;
@@ -795,7 +814,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graphs(c);
     c->jit.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->mpuMasks, c->offs, c->vq, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -812,6 +831,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
     else if (option == PSGPU_OPT_DEBUG) c->debug = (int)value;
     else if (option == PSGPU_OPT_GRAPH) c->useGraph = value != 0;
+    else if (option == PSGPU_OPT_BOUND) c->bound = value != 0;
     else if (option == PSGPU_OPT_CAPACITY && value >= 64 && value <= (1ll << 30)) {
         // restart the output / work-queue buffers at this vertex capacity (they grow on demand)
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
@@ -936,7 +956,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             V += h.shard[k].v;
             T += h.shard[k].t;
             S += h.shard[k].s;
-            P += h.shard[k].p;
+            P += h.shard[k].p + h.shard[k].b;
         }
         PsMeshInfo& I = c->info;
         memset(&I, 0, sizeof(I));
@@ -993,17 +1013,14 @@ int psgpu_download_mesh(psgpu_ctx* c, float* pos, float* nrm, float* col, uint32
 }
 
 namespace {
-// S1 survivors of the last run (global ids, ascending), gathered from the shard queues.
+// S1 survivors of the last run (global ids, ascending), from the per-MPU flags.
 int survivors(psgpu_ctx* c, std::vector<uint32_t>& ids) {
     ids.clear();
     if (!c->mpuCount) return PSGPU_RET_SUCCESS;
-    const DevCounters& h = *c->hostCtr;
-    std::vector<uint32_t> all((size_t)c->pShardCap * kShards);
-    PSGPU_CHECK(hipMemcpy(all.data(), c->pq, all.size() * 4, hipMemcpyDeviceToHost));
-    for (int k = 0; k < kShards; ++k)
-        ids.insert(ids.end(), all.begin() + (size_t)k * c->pShardCap,
-                   all.begin() + (size_t)k * c->pShardCap + std::min(h.shard[k].p, c->pShardCap));
-    std::sort(ids.begin(), ids.end());
+    std::vector<uint8_t> passed(c->mpuCount);
+    PSGPU_CHECK(hipMemcpy(passed.data(), c->passed, passed.size(), hipMemcpyDeviceToHost));
+    for (uint32_t l = 0; l < c->mpuCount; ++l)
+        if (passed[l]) ids.push_back(c->mpuBegin + l);
     return PSGPU_RET_SUCCESS;
 }
 }  // namespace

@@ -122,7 +122,8 @@ struct DevModel {
     uint32_t nSlots;
     uint32_t ctPrims;
     uint32_t ctOps;
-    uint32_t pad[4];
+    uint32_t boundable;  // 1: field bounds over a box are valid (see prim_bound, psgpu_device.h)
+    uint32_t pad[3];
     Instr instr[kMaxInstr];
     DevOp ops[128];
     DevPrim prims[128];
@@ -156,7 +157,8 @@ struct ShardCtr {           // one 128-B line per shard: atomics on one line ser
     uint32_t v;             // vertex records appended
     uint32_t t;             // triangle records appended
     uint32_t s;             // surface MPUs (>= 1 triangle)
-    uint32_t pad[28];
+    uint32_t b;             // S1 survivors proven empty by field bounds (not queued)
+    uint32_t pad[27];
 };
 struct DevCounters {
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
@@ -182,6 +184,8 @@ struct Params {
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
+    uint8_t* passed;        // mpuCount: 1 if the MPU passed S1 (PsMpuStats::passedPrecheck)
+    uint32_t bound;         // k_precheck proves S1 survivors empty by field bounds
     uint64_t* mpuMasks;     // 2 * mpuCount: culling mask of each surface MPU's box + delta
     uint64_t* offs;         // mpuCount + 1: exclusive scan of counts
     uint64_t* scanStatus;   // offsets-scan look-back words of this run (zeroed by the previous run)

@@ -53,6 +53,7 @@ OPT_VERTEX_BLOCKS_PER_CU = 4
 OPT_FINISH_BLOCKS_PER_CU = 5
 OPT_CAPACITY = 6
 OPT_GRAPH = 7
+OPT_BOUND = 10
 
 
 def load(build_if_missing: bool = True):
