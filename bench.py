@@ -255,7 +255,7 @@ def main():
                      "valu_issue_util": valu_util, "valu_source": valu_src},
         "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
         "mesh": {"vertices": info.ctVertices, "triangles": info.ctTriangles, "passed_s1": info.ctPassedPrecheck,
-                 "surface_mpus": info.ctSurfaceMPUs, "per_rank": counts},
+                 "surface_mpus": info.ctSurfaceMPUs, "field_mpus": info.ctFieldMPUs, "per_rank": counts},
         "hbm_gbs_algorithmic": round((info.ctVertices * 36 + info.ctTriangles * 12) / (ms_step * 1e-3) / 1e9, 2),
     }
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:

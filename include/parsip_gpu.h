@@ -144,6 +144,9 @@ typedef struct PsMeshInfo {
     uint32_t ctTriangles;
     int32_t  firstOverflowMPU;  /* global MPU id with > 512 V or T, or -1           */
     uint64_t ctLaneEvals;       /* field evaluations performed (per point)          */
+    uint32_t ctFieldMPUs;       /* S1 survivors whose 8^3 field cache was evaluated
+                                 * (the rest were proven empty by field bounds)     */
+    uint32_t reserved;
 } PsMeshInfo;
 
 /* Device-resident compact mesh of the last polygonization (pointers into the

@@ -951,12 +951,13 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             fprintf(stderr, "psgpu: device protocol error 0x%x\n", h.error);
             return PSGPU_RET_DEVICE_ERROR;
         }
-        uint32_t V = 0, T = 0, S = 0, P = 0;
+        uint32_t V = 0, T = 0, S = 0, P = 0, Q = 0;
         for (int k = 0; k < kShards; ++k) {
             V += h.shard[k].v;
             T += h.shard[k].t;
             S += h.shard[k].s;
             P += h.shard[k].p + h.shard[k].b;
+            Q += h.shard[k].p;
         }
         PsMeshInfo& I = c->info;
         memset(&I, 0, sizeof(I));
@@ -966,7 +967,8 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         I.ctVertices = c->mpuCount ? V : 0;
         I.ctTriangles = c->mpuCount ? T : 0;
         I.firstOverflowMPU = (c->mpuCount && h.firstOverflow != 0x7fffffff) ? h.firstOverflow : -1;
-        I.ctLaneEvals = 8ull * c->mpuCount + 512ull * I.ctPassedPrecheck + 8ull * I.ctVertices;
+        I.ctFieldMPUs = c->mpuCount ? Q : 0;
+        I.ctLaneEvals = 8ull * c->mpuCount + 512ull * I.ctFieldMPUs + 8ull * I.ctVertices;
         c->haveResult = true;
     }
     if (!c->haveResult) return PSGPU_RET_PARAM_ERROR;

@@ -30,7 +30,8 @@ class PsMeshInfo(ctypes.Structure):
     _fields_ = [("ctMPUs", ctypes.c_uint32), ("ctPassedPrecheck", ctypes.c_uint32),
                 ("ctSurfaceMPUs", ctypes.c_uint32), ("ctVertices", ctypes.c_uint32),
                 ("ctTriangles", ctypes.c_uint32), ("firstOverflowMPU", ctypes.c_int32),
-                ("ctLaneEvals", ctypes.c_uint64)]
+                ("ctLaneEvals", ctypes.c_uint64), ("ctFieldMPUs", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class PsMeshDevice(ctypes.Structure):

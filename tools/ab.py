@@ -36,7 +36,9 @@ def main():
             p.set_option(OPT[k], int(val))
         p.set_model(model)
         os.environ.pop("PSGPU_JIT_FLAGS", None)
-        p.run(cs)
+        info = p.run(cs)
+        print(f"{v:28s} V={info.ctVertices} T={info.ctTriangles} passedS1={info.ctPassedPrecheck} "
+              f"fieldMPUs={info.ctFieldMPUs} surface={info.ctSurfaceMPUs}", flush=True)
         polys.append(p)
     kt = {v: {} for v in a.variants}
     step = {v: [] for v in a.variants}
