@@ -835,7 +835,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     qv = lane_value(qv, 0);
     qt = lane_value(qt, 0);
     if (p.cull && V > 0u) {  // culling mask of the MPU box grown by the normal delta, for k_vertex
-        const float e = 7.0f * cs + 0.001f;
+        const float e = 7.0f * cs + 0.001f;  // and k_finish (edge samples, roots, normal samples)
         const CullMask cg = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
         if (lane == 0) {
             p.mpuMasks[2 * w] = cg.lo;
@@ -1109,16 +1109,32 @@ __device__ __forceinline__ CullMask cull_mask_points_n(ModelPtr M, const float* 
                          wave_max(z1) + ext);
 }
 
+// Culling mask of a wave whose lanes hold points of the MPUs w (range slots): the AND of
+// those MPUs' masks (k_mpu, box grown by the normal delta), one scalar load pair per
+// distinct MPU.  A primitive culled for every one of the boxes is +0 at all the points.
+__device__ __forceinline__ CullMask cull_mask_mpus(const Params& p, uint32_t w) {
+    CullMask cm{~0ull, ~0ull};
+    bool todo = true;
+    for (;;) {
+        const uint64_t b = ballot(todo);
+        if (b == 0ull) break;
+        const uint32_t w0 = lane_value(w, (int)__builtin_ctzll(b));
+        cm.lo &= p.mpuMasks[2 * w0];
+        cm.hi &= p.mpuMasks[2 * w0 + 1];
+        if (w == w0) todo = false;
+    }
+    return cm;
+}
+
 #ifndef PSGPU_V_N
 #define PSGPU_V_N 1  // vertices per quad of lanes per k_vertex pass (2: bigger culling boxes, slower)
 #endif
 
 // Vertices: 16 * VN per wavefront pass, one quad of lanes per vertex and VN vertices
 // per quad (vertex first + quad + 16n), each walk evaluating VN points per lane.
-// Phase A (quad pruning): the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762)
-// Phase B (per-lane pruning): lane 0 = p, lanes 1..3 = p + delta*e_a
-// (fieldValueAndColor's value + normal, :764-807; the colour walk runs in k_finish).
-// Position and normal go into the vertex record; k_finish places them in the mesh.
+// Quad pruning: the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762), then the
+// linear root.  The position goes into the vertex record; k_finish evaluates value,
+// colour and normal there (:764-807) and places the vertex in the mesh.
 template <class EV>
 __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     constexpr int VN = PSGPU_V_N;
@@ -1129,8 +1145,6 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const float third = 1.0f / 3.0f;
     const int j = lane & 3;
     const float r = (float)j * third;
-    const float delta = 0.001f;
-    const float inv = -1.0f / delta;
     const float cs = p.cs;
     if (blockIdx.x < p.scanBlocks) scan_counts_block(p, blockIdx.x);  // block-uniform
     const ShardBatches sb(&p.ctr->shard[0].v, p.vShardCap, 16 * VN);
@@ -1167,20 +1181,15 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             qy[n] = e1y[n] + dY[n] * r;
             qz[n] = e1z[n] + dZ[n] * r;
         }
-        // the edge samples' AABB grown by delta also covers p + delta*e_a whenever p lies on
-        // the bracketing segment (0 <= scale <= 1); phase B recomputes the mask otherwise
-        // one MPU in the whole pass: its box grown by delta (k_mpu's mask) covers every sample
-        // and, while the roots stay on their segments, every normal sample
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane(wrec[0]);
-        bool oneMpu = true;
-#pragma unroll
-        for (int n = 0; n < VN; ++n) oneMpu = oneMpu && wrec[n] == w0;
-        CullMask cm;
-        if (p.cull && ballot(!oneMpu) == 0ull) {
-            cm.lo = p.mpuMasks[2 * w0];
-            cm.hi = p.mpuMasks[2 * w0 + 1];
-        } else {
-            cm = cull_mask_points_n<VN>(M, qx, qy, qz, p.cull != 0, delta);
+        // every edge sample lies in its MPU's box (k_mpu's mask; the d^2 >= 1.02 margin
+        // absorbs the last-bit rounding of e1 + cs vs lo + 7 cs)
+        CullMask cm{0ull, 0ull};
+        if (p.cull) {
+            if (VN == 1) {
+                cm = cull_mask_mpus(p, wrec[0]);
+            } else {
+                cm = cull_mask_points_n<VN>(M, qx, qy, qz, true);
+            }
         }
         float f[VN];
         if (p.debug & 256u) {  // ablation bit 8: no phase-A walk
@@ -1189,8 +1198,6 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
         } else {
             ev.template evaln<4, false, VN>(qx, qy, qz, cm, f, nullptr);
         }
-        float P0[VN], P1[VN], P2[VN], qx2[VN], qy2[VN], qz2[VN];
-        bool offEdge = false;
 #pragma unroll
         for (int n = 0; n < VN; ++n) {
             float fs[4], xs[4], ys[4], zs[4];
@@ -1217,45 +1224,22 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
             const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
             const float scale = (0.5f - fa) / (fb - fa);
-            P0[n] = ax0 + scale * (bx0 - ax0);
-            P1[n] = ay0 + scale * (by0 - ay0);
-            P2[n] = az0 + scale * (bz0 - az0);
-            qx2[n] = j == 1 ? P0[n] + delta : P0[n];
-            qy2[n] = j == 2 ? P1[n] + delta : P1[n];
-            qz2[n] = j == 3 ? P2[n] + delta : P2[n];
-            // p off its edge (no sign change in the samples, or inf/NaN)
-            offEdge = offEdge || (valid[n] && !(scale >= 0.0f && scale <= 1.0f));
-        }
-        // fieldValue at p and at the three normal samples
-        const CullMask cmB = ballot(offEdge) == 0ull ? cm : cull_mask_points_n<VN>(M, qx2, qy2, qz2, p.cull != 0);
-        float g[VN];
-        if (p.debug & 128u) {  // ablation bit 7: no phase-B walk
-#pragma unroll
-            for (int n = 0; n < VN; ++n) g[n] = f[n];
-        } else {
-            ev.template evaln<1, false, VN>(qx2, qy2, qz2, cmB, g, nullptr);
-        }
-#pragma unroll
-        for (int n = 0; n < VN; ++n) {
-            const float vtx = quad_bcast<0>(g[n]);
-            const float gx = quad_bcast<1>(g[n]), gy = quad_bcast<2>(g[n]), gz = quad_bcast<3>(g[n]);
-            float nx = (gx - vtx) * inv, ny = (gy - vtx) * inv, nz = (gz - vtx) * inv;
-            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);  // SimdNormalize
-            nx = nx * im;
-            ny = ny * im;
-            nz = nz * im;
-            if (valid[n] && j == 0) {  // into the record; k_finish places it in the mesh
+            if (valid[n] && j == 0) {  // into the record; k_finish adds normal and colour
                 VertexRec& out = p.vq[rec[n]];
-                out.pos[0] = P0[n]; out.pos[1] = P1[n]; out.pos[2] = P2[n];
-                out.nrm[0] = nx; out.nrm[1] = ny; out.nrm[2] = nz;
+                out.pos[0] = ax0 + scale * (bx0 - ax0);
+                out.pos[1] = ay0 + scale * (by0 - ay0);
+                out.pos[2] = az0 + scale * (bz0 - az0);
+                // 1: p lies on its bracketing segment, inside the MPU box (no inf/NaN)
+                out.nrm[0] = (scale >= 0.0f && scale <= 1.0f) ? 1.0f : 0.0f;
             }
         }
     }
 }
 
-// Finish: vertex colours (fieldValueAndColor's colour walk at every vertex position,
-// PS_Polygonizer.cpp:777-778, 1378-1551; one lane per vertex, 64 per wave), then the
-// triangle records -> global vertex ids.  Runs after k_vertex wrote the positions.
+// Finish: per vertex (one lane per vertex, 64 per wave) fieldValueAndColor's value and
+// colour walk (PS_Polygonizer.cpp:777-778, 1378-1551) and the three normal samples
+// (:780-781, 1598-1622), then the triangle records -> global vertex ids.  Runs after
+// k_vertex wrote the positions.
 template <class EV>
 __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
@@ -1264,6 +1248,8 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
+    const float delta = 0.001f;
+    const float inv = -1.0f / delta;
     if (blockIdx.x == 0) {  // the run's counters for the host (mapped pinned memory)
         const uint32_t* src = reinterpret_cast<const uint32_t*>(p.ctr);
         uint32_t* dst = reinterpret_cast<uint32_t*>(p.hostCtr);
@@ -1284,17 +1270,42 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         const VertexRec R = p.vq[(size_t)shard * p.vShardCap + rec];
         const uint32_t gi = (uint32_t)p.offs[R.w] + (R.vidKey & 0xffffu);
         float c[3] = {0.0f, 0.0f, 0.0f};
-        if (!(p.debug & 32u)) {  // ablation bit 5: no colour walk
-            const CullMask cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], p.cull != 0);
-            (void)ev.template eval<1, true>(R.pos[0], R.pos[1], R.pos[2], cm, c);
+        float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        if (!(p.debug & 32u)) {  // ablation bit 5: no walks
+            // vertices on their segments: the MPU masks (boxes grown by delta) cover p and
+            // every normal sample; otherwise the wave's own box grown by delta
+            CullMask cm{0ull, 0ull};
+            if (p.cull) {
+                if (ballot(!(R.nrm[0] == 1.0f)) == 0ull) cm = cull_mask_mpus(p, R.w);
+                else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
+            }
+            // value + colour at p and the normal's per-point fieldValue at p + delta*e_a
+            // (:1598-1622) as four points of one walk (the colour of points 1-3 is dead
+            // code); then SimdNormalize (rsqrt -> IEEE 1/sqrtf)
+            const float qx[4] = {R.pos[0], R.pos[0] + delta, R.pos[0], R.pos[0]};
+            const float qy[4] = {R.pos[1], R.pos[1], R.pos[1] + delta, R.pos[1]};
+            const float qz[4] = {R.pos[2], R.pos[2], R.pos[2], R.pos[2] + delta};
+            float g[4], c4[12];
+            ev.template evaln<1, true, 4>(qx, qy, qz, cm, g, c4);
+            c[0] = c4[0];
+            c[1] = c4[1];
+            c[2] = c4[2];
+            const float vtx = g[0];
+            nx = (g[1] - vtx) * inv;
+            ny = (g[2] - vtx) * inv;
+            nz = (g[3] - vtx) * inv;
+            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);
+            nx = nx * im;
+            ny = ny * im;
+            nz = nz * im;
         }
         if (valid && gi < p.vCap) {  // past vCap: finish() grows and re-runs
             p.pos[gi * 3 + 0] = R.pos[0];
             p.pos[gi * 3 + 1] = R.pos[1];
             p.pos[gi * 3 + 2] = R.pos[2];
-            p.nrm[gi * 3 + 0] = R.nrm[0];
-            p.nrm[gi * 3 + 1] = R.nrm[1];
-            p.nrm[gi * 3 + 2] = R.nrm[2];
+            p.nrm[gi * 3 + 0] = nx;
+            p.nrm[gi * 3 + 1] = ny;
+            p.nrm[gi * 3 + 2] = nz;
             p.col[gi * 3 + 0] = c[0];
             p.col[gi * 3 + 1] = c[1];
             p.col[gi * 3 + 2] = c[2];

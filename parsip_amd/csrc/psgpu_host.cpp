@@ -384,7 +384,7 @@ struct psgpu_ctx {
     int cull = 1;
     int debug = 0;
     int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
-    int finishBlocksPerCU = 4;
+    int finishBlocksPerCU = 8;
     int timing = 0;
     // geometry of the last run
     float cs = 0.0f;
