@@ -691,17 +691,17 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
 #define PSGPU_S2_N 8  // x-slices per walk in S2 (1, 2, 4 or 8): one walk per (y,z) needle
                       // shares each primitive's uniform work and (y,z) terms over 8 points
 #endif
-constexpr int kLdsFv = 0;
-constexpr int kLdsEdge = 0;  // edgeVid reuses the field cache: fv is dead after pass 1
+constexpr int kLdsEdge = 0;
 constexpr int kLdsCfg = kLdsEdge + 1536 * 2;
 constexpr int kLdsVbase = kLdsCfg + 344;
 constexpr int kLdsTbase = kLdsVbase + 344 * 2;
 constexpr int kLdsSlots = ((kLdsTbase + 344 * 2) + 15) & ~15;
 
 // Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
-// LDS per block: the packed cube tables (shared), then per wave: fv[512] f32 (S2, pass 1)
-// aliased by edgeVid[1536] u16 (passes 2-3; the wavefront fence after pass 1 orders the
-// two) | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots (interpreter).
+// LDS per block: the packed cube tables (shared), then per wave: edgeVid[1536] u16
+// (passes 2-3) | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots
+// (interpreter).  The S2 field cache never leaves registers: pass 1 needs only its
+// inside bits (8 ballots).
 constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
 
 // Last cell c in [0, 343) with first[c] <= r (first[] = exclusive prefix of per-cell
@@ -737,7 +737,6 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     __syncthreads();
     if (pidx >= pcount) return;
     unsigned char* base = smem + kLdsTables + wave * (kLdsSlots + p.slotsPerLane * 64 * 4);
-    float* fv = reinterpret_cast<float*>(base + kLdsFv);
     uint16_t* edgeVid = reinterpret_cast<uint16_t*>(base + kLdsEdge);
     uint8_t* cellCfg = base + kLdsCfg;
     uint16_t* cellV = reinterpret_cast<uint16_t*>(base + kLdsVbase);
@@ -751,7 +750,8 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     mpu_origin(p, m, o);
     const float cs = p.cs;
 
-    // S2 (:550-610): fv[x][y][z], lane = y*8 + z; quads = 4 consecutive z
+    // S2 (:550-610): corner (x, y, z) of the 8x8x8 cache, lane = y*8 + z, 8 x per lane;
+    // quads = 4 consecutive z
     const int y = lane >> 3, z = lane & 7;
     const float py = o[1] + (float)y * cs;
     const float pz = o[2] + (float)z * cs;
@@ -777,35 +777,34 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
     for (int h = 0; h < 8; h += PSGPU_S2_N)
         ev.template evaln<4, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs8 + h, nullptr);
 #endif
+    // inside bits of the 8x8x8 corners: ins[x] bit y*8 + z (lane order)
+    uint64_t ins[8];
     uint32_t inside = 0;
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
-        fv[x * 64 + lane] = fs8[x];
-        inside += __popcll(ballot(fs8[x] >= 0.5f));
+        ins[x] = ballot(fs8[x] >= 0.5f);
+        inside += __popcll(ins[x]);
     }
     if (inside == 0 || inside == 512 || (p.debug & 1u)) {  // no vertices, no triangles
         if (lane == 0) p.counts[w] = 0ull;
         return;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
 
     // S3 pass 1 (:647-691): config per cell (bit c = x*4 + y*2 + z, inside = f >= 0.5),
     // owned sign-changing edges (new vertices) and triangles; wave prefix sums give
-    // the reference's discovery order over cells (i,j,k)
+    // the reference's discovery order over cells (i,j,k): one x-slab i per step, lane
+    // j*8 + k, so the cell's corners are bits lane + {0, 1, 8, 9} of ins[i] and ins[i+1]
     const uint64_t edgeBits = tab->edge;
     uint32_t carryV = 0, carryT = 0;
-    for (int q = 0; q < 6; ++q) {
-        const int c = q * 64 + lane;
-        const int i = c / 49, j = (c / 7) % 7, k = c % 7;
-        uint32_t cfg = 0;
-        if (c < 343) {
+    const int j = lane >> 3, k = lane & 7;
+    const bool cellLane = j < 7 && k < 7;
 #pragma unroll
-            for (int cc = 0; cc < 8; ++cc) {
-                const int xx = i + ((cc >> 2) & 1), yy = j + ((cc >> 1) & 1), zz = k + (cc & 1);
-                cfg |= (fv[xx * 64 + yy * 8 + zz] >= 0.5f ? 1u : 0u) << cc;
-            }
-        }
+    for (int i = 0; i < 7; ++i) {
+        const int c = i * 49 + j * 7 + k;
+        const uint32_t b0 = (uint32_t)(ins[i] >> lane), b1 = (uint32_t)(ins[i + 1] >> lane);
+        uint32_t cfg = 0;
+        if (cellLane)
+            cfg = (b0 & 3u) | ((b0 >> 6) & 12u) | ((b1 & 3u) << 4) | (((b1 >> 8) & 3u) << 6);
         uint32_t nv = 0, nt = 0;
         if (cfg != 0 && cfg != 255) {
             const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
@@ -814,7 +813,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
         }
         const uint32_t sv = wave_incl_scan(nv);
         const uint32_t st = wave_incl_scan(nt);
-        if (c < 343) {
+        if (cellLane) {
             cellCfg[c] = (uint8_t)cfg;
             cellV[c] = (uint16_t)(carryV + sv - nv);
             cellT[c] = (uint16_t)(carryT + st - nt);
