@@ -3,16 +3,17 @@
 // Pipeline for one polygonization of MPUs [begin, begin+count) (the reference's
 // Polygonize + CMPUProcessor, PS_Polygonizer.cpp:315-385, 441-829):
 //
-//   k_precheck  8 lanes per MPU, 2 quads: S1 corner test F>0          (:483-540), and the
-//               ordered list of the MPUs that passed (single-pass look-back compaction)
-//   k_mpu       one wavefront per passing MPU: S2 8^3 field cache in LDS (quads of 4
-//               z-consecutive corners), S3 configs, vertex ownership + wave prefix
-//               sums for the reference's discovery order, triangle records
-//   (k_vertex)  its first blocks also scan the per-MPU counts into mesh offsets
-//   k_vertex    one quad per vertex: S4 4-sample root bracket, S5 colour + normals
-//   k_finish    vertex colours (64 per wave) + triangle records -> global vertex ids
+//   k_precheck  8 lanes per MPU, 2 quads: S1 corner test F>0          (:483-540); field
+//               bounds per octant prove surface-free survivors; the rest are queued
+//   k_mpu       one wavefront per queued survivor: S2 inside bits of the 8^3 corners
+//               (quads of 4 z-consecutive corners), S3 configs, vertex ownership + wave
+//               prefix sums for the reference's discovery order, vertex / triangle records
+//   k_vertex    its first blocks scan the per-MPU counts into mesh offsets; then one
+//               quad per vertex: S4 4-sample root bracket and linear root
+//   k_finish    one lane per vertex: S5 value + colour + 3 normal samples as one 4-point
+//               walk, the compact mesh; triangle records -> global vertex ids
 //
-// The tree-evaluating kernels (precheck, mpu, vertex, probe) exist twice: here with
+// The tree-evaluating kernels (precheck, mpu, vertex, finish, probe) exist twice: here with
 // the generic walk-program interpreter (InterpEval), and specialised per model
 // structure at run time by psgpu_jit.cpp (hiprtc), which the host prefers.  Both
 // instantiate the same bodies from psgpu_device.h.
