@@ -232,6 +232,9 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        output unchanged; JIT kernels only) */
 #define PSGPU_OPT_JIT           3   /* 0 interpreter, 1 specialised per structure (default),
                                        2 specialised with parameters baked in */
+#define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the
+                                       specialised kernels on a host thread while the interpreter
+                                       serves polygonizations (bit-identical output); 0: block */
 /* Host-only (no GPU): compile the model's specialised kernels with hiprtc (mode 1:
  * structure only, 2: parameters baked in); returns the code-object size or a negative
  * error (log receives the compiler output). */
@@ -239,6 +242,11 @@ long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mat
                        const PsSoaBlobOps* ops, int mode, char* log, size_t cap);
 /* 1 if the current model runs on run-time specialised kernels, 0 on the interpreter. */
 int  psgpu_jit_active(psgpu_ctx* ctx);
+/* 1 while the current model's specialised kernels are still compiling. */
+int  psgpu_jit_pending(psgpu_ctx* ctx);
+/* Block until the current model's compile has finished and adopt its kernels; returns
+ * psgpu_jit_active afterwards (0: the compile failed and the interpreter stays). */
+int  psgpu_jit_wait(psgpu_ctx* ctx);
 /* Generated specialised HIP source of the current model; returns its length. */
 int  psgpu_jit_source(psgpu_ctx* ctx, char* buf, size_t cap);
 

@@ -101,7 +101,9 @@ inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, cons
                                          detail::as_c<Mats, PsSoaPrimMatrices>(mats),
                                          detail::as_c<Ops, PsSoaBlobOps>(ops),
                                          reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr);
-    polyMPUs.ctMPUs = ct < capacity ? ct : capacity;
+    // on failure nothing was exported: report no MPUs (SimdPoly::draw walks ctMPUs,
+    // PS_HighPerformanceRender.cpp:378-426, and must not draw stale ones)
+    polyMPUs.ctMPUs = rc == PSGPU_RET_SUCCESS ? ct : 0u;
     return rc;
 }
 

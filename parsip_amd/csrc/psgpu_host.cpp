@@ -11,7 +11,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -244,13 +246,17 @@ int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, con
     // Colour of each op whose subtree is all +0 fields (culled primitives, or pruned: the
     // reference's colour pass then reads zeroed arrays, :1472-1522): a constant of the tree
     // and the primitive colours, computed in fp32 exactly as op_colour_weights + the
-    // weighted sum on the device.  Ops are numbered pre-order: children have larger ids.
-    for (int op = (int)O.ctOps - 1; op >= 0; --op) {
+    // weighted sum on the device.  Children first (post-order over the tree the program
+    // builder validated: every child op id < ctOps, every prim id < 128, no cycles), so any
+    // op numbering works, not only pre-order; unreachable ops keep zero.
+    const float* pc[3] = {P.colorX, P.colorY, P.colorZ};
+    std::function<void(int)> zero_col = [&](int op) {
         const uint32_t t = O.opType[op], kind = O.opChildKind[op];
         const uint32_t L = O.opLeftChild[op], R = O.opRightChild[op];
+        if (kind & 2) zero_col((int)L);
+        if (kind & 1) zero_col((int)R);
         float cl[3], cr[3];
         for (int k = 0; k < 3; ++k) {
-            const float* pc[3] = {P.colorX, P.colorY, P.colorZ};
             cl[k] = (kind & 2) ? D.zeroCol[L][k] : pc[k][L];
             cr[k] = (kind & 1) ? D.zeroCol[R][k] : pc[k][R];
         }
@@ -270,7 +276,8 @@ int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, con
             else if (t >= PSGPU_OP_WARPTWIST && t <= PSGPU_OP_WARPSHEAR) D.zeroCol[op][k] = cl[k];
             else D.zeroCol[op][k] = 0.0f;  // not used: zero subtrees contain only the types above
         }
-    }
+    };
+    if (O.ctOps > 0) zero_col(0);
     // every one of the 128 prim slots is uploaded: the reference evaluates whatever
     // index an op names, even past ctPrims (SOABlobPrims keeps all 128 entries)
     for (uint32_t i = 0; i < 128; ++i) {
@@ -378,7 +385,10 @@ struct psgpu_ctx {
     DevModel* dModel = nullptr;
     CubeTablesDev* dTables = nullptr;
     int useJit = 1;
+    int jitAsync = 1;                  // set_model returns while hiprtc compiles (interpreter meanwhile)
     std::shared_ptr<JitKernels> jit;   // specialised kernels of the current model
+    JitFuture jitFut;                  // the current model's compile, while jitPending
+    bool jitPending = false;
     std::string jitError;
     bool haveModel = false;
     int cull = 1;
@@ -427,6 +437,9 @@ struct psgpu_ctx {
     } graphs[2];
     float lastMs[kNumKernels] = {};
     PsMeshInfo info{};
+    // high-water marks of finished runs: the next run's buffers are sized from them
+    // (an animation whose mesh grows frame to frame does not pay a synchronous re-run)
+    uint32_t seenV = 0, seenT = 0, seenShardV = 0, seenShardT = 0;
 };
 
 namespace {
@@ -566,6 +579,7 @@ void drop_graphs(psgpu_ctx* c) {
 // (k_finish of the previous run reset this run's counters) and k_finish publishes the
 // counters to mapped host memory.  Replayed from a hipGraph (one per counter set) while
 // the launch parameters repeat, e.g. per frame of an animation.
+void reset_run_state(psgpu_ctx* c);
 int enqueue(psgpu_ctx* c, hipStream_t s) {
     if (c->mpuCount == 0) {  // nothing to launch: an empty result
         memset(c->hostCtr, 0, sizeof(DevCounters));
@@ -576,7 +590,11 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     const uint32_t slot = c->parity;
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool timed = c->timing != 0;
-    if (!c->useGraph || timed || s == nullptr) return launch_all(c, p, s, timed);
+    if (!c->useGraph || timed || s == nullptr) {
+        const int rc = launch_all(c, p, s, timed);
+        if (rc != PSGPU_RET_SUCCESS) reset_run_state(c);
+        return rc;
+    }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
     const uint32_t shape[3] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
@@ -589,6 +607,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         const hipError_t ec = hipStreamEndCapture(s, &graph);
         if (rc != PSGPU_RET_SUCCESS) {
             if (graph) (void)hipGraphDestroy(graph);
+            reset_run_state(c);
             return rc;
         }
         PSGPU_CHECK(ec);
@@ -604,6 +623,53 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
 }
 
 int set_device(psgpu_ctx* c) { return hip_fail(hipSetDevice(c->device), "hipSetDevice"); }
+
+// Adopt the model's specialised kernels once their compile has finished (wait: block for
+// it).  Until then the interpreter runs; its output is bit-identical.  Call with the
+// context's device current.
+void jit_poll(psgpu_ctx* c, bool wait) {
+    if (!c->jitPending) return;
+    if (!wait && c->jitFut.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return;
+    std::shared_ptr<const JitCode> code = c->jitFut.get();
+    c->jitPending = false;
+    c->jitFut = JitFuture();
+    if (c->pending) (void)hipStreamSynchronize(c->runStream);
+    drop_graphs(c);
+    c->jit = jit_load(*code, c->device, &c->jitError);
+    if (!c->jit && code->code.size() && c->jitError.find("dropped") != std::string::npos) {
+        // the cached object would not load: compile it afresh (bypassing the disk cache)
+        c->jitFut = jit_request(c->model, c->useJit == 2, false);
+        c->jitPending = true;
+        if (wait) jit_poll(c, true);
+        return;
+    }
+    if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
+}
+
+// Start (or restart) the compile of the current model's kernels.
+void jit_start(psgpu_ctx* c) {
+    c->jit.reset();
+    c->jitPending = false;
+    c->jitFut = JitFuture();
+    if (!c->useJit || !c->haveModel) return;
+    c->jitFut = jit_request(c->model, c->useJit == 2);
+    c->jitPending = true;
+    jit_poll(c, !c->jitAsync);
+}
+
+// Put a context whose launch sequence failed part-way back into a usable state: the
+// next run's counters and look-back words were to be reset by this run's k_finish.
+void reset_run_state(psgpu_ctx* c) {
+    DevCounters init[2];
+    memset(init, 0, sizeof(init));
+    init[0].firstOverflow = init[1].firstOverflow = 0x7fffffff;
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipMemcpy(c->ctr, init, sizeof(init), hipMemcpyHostToDevice);
+    (void)hipMemset(c->scanStatus, 0, 2 * kScanMaxBlocks * sizeof(uint64_t));
+    (void)hipDeviceSynchronize();
+    c->parity = 0;
+    drop_graphs(c);
+}
 
 }  // namespace
 
@@ -827,14 +893,19 @@ void psgpu_destroy(psgpu_ctx* c) {
 
 int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     if (!c) return PSGPU_RET_PARAM_ERROR;
+    const int drc = set_device(c);  // modules load and buffers free on the context's device
+    if (drc != PSGPU_RET_SUCCESS) return drc;
     if (option == PSGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
     else if (option == PSGPU_OPT_CULLING) c->cull = value != 0;
     else if (option == PSGPU_OPT_DEBUG) c->debug = (int)value;
     else if (option == PSGPU_OPT_GRAPH) c->useGraph = value != 0;
     else if (option == PSGPU_OPT_BOUND) c->bound = value != 0;
     else if (option == PSGPU_OPT_CAPACITY && value >= 64 && value <= (1ll << 30)) {
-        // restart the output / work-queue buffers at this vertex capacity (they grow on demand)
+        // restart the output / work-queue buffers at this vertex capacity (they grow on demand);
+        // a pending result is dropped with them
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
+        c->pending = false;
+        c->seenV = c->seenT = c->seenShardV = c->seenShardT = 0;
         void* bufs[] = {c->vq, c->tq, c->pos, c->nrm, c->col, c->tris};
         for (void* b : bufs)
             if (b) (void)hipFree(b);
@@ -853,12 +924,9 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         c->useJit = (int)value;
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
         drop_graphs(c);
-        if (!c->useJit) c->jit.reset();
-        else if (c->haveModel) {
-            c->jit = jit_get(c->model, c->useJit == 2, c->device, &c->jitError);
-            if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
-        }
+        jit_start(c);
     }
+    else if (option == PSGPU_OPT_JIT_ASYNC) c->jitAsync = value != 0;
     else return PSGPU_RET_PARAM_ERROR;
     return PSGPU_RET_SUCCESS;
 }
@@ -880,11 +948,7 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
     PSGPU_CHECK(hipStreamSynchronize(c->stream));
     c->haveModel = true;
-    c->jit.reset();
-    if (c->useJit) {
-        c->jit = jit_get(c->model, c->useJit == 2, c->device, &c->jitError);
-        if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
-    }
+    jit_start(c);
     return PSGPU_RET_SUCCESS;
 }
 
@@ -902,6 +966,13 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     const uint32_t end = (uint32_t)std::min<uint64_t>(mpuEnd, total);
     c->mpuBegin = std::min(mpuBegin, end);
     c->mpuCount = end - c->mpuBegin;
+    jit_poll(c, false);
+    // capacity from the largest finished run + 1/4 (grows only; finish() still re-runs
+    // on an overflow, so a prediction that falls short costs time, never output)
+    c->vcap = std::max(c->vcap, c->seenV + c->seenV / 4);
+    c->tcap = std::max(c->tcap, c->seenT + c->seenT / 4);
+    c->vShardCap = std::max(c->vShardCap, c->seenShardV + c->seenShardV / 4);
+    c->tShardCap = std::max(c->tShardCap, c->seenShardT + c->seenShardT / 4);
     rc = ensure_buffers(c, c->mpuCount);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     rc = enqueue(c, s);
@@ -929,7 +1000,12 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
                 mv = std::max(mv, h.shard[k].v);
                 mt = std::max(mt, h.shard[k].t);
             }
+            c->seenV = std::max(c->seenV, V);
+            c->seenT = std::max(c->seenT, T);
+            c->seenShardV = std::max(c->seenShardV, mv);
+            c->seenShardT = std::max(c->seenShardT, mt);
             if (V <= c->vcap && T <= c->tcap && mv <= c->vShardCap && mt <= c->tShardCap) break;
+            if (attempt == 3) return PSGPU_RET_NOT_ENOUGH_MEM;  // still short after 3 regrowths
             c->vcap = std::max(c->vcap, V + V / 8 + 1024);
             c->tcap = std::max(c->tcap, T + T / 8 + 1024);
             c->vShardCap = std::max(c->vShardCap, mv + mv / 4 + 256);
@@ -1112,6 +1188,7 @@ int psgpu_field_values(psgpu_ctx* c, const float* xyz, uint32_t n, int mode, flo
     if (!c || !c->haveModel || !xyz || !out || mode < 0 || mode > 2) return PSGPU_RET_PARAM_ERROR;
     int rc = set_device(c);
     if (rc != PSGPU_RET_SUCCESS) return rc;
+    jit_poll(c, false);
     if (n == 0) return PSGPU_RET_SUCCESS;
     float *dx = nullptr, *dout = nullptr, *dcol = nullptr;
     PSGPU_CHECK(hipMalloc(&dx, (size_t)n * 12));
@@ -1154,7 +1231,23 @@ long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mat
 }
 
 // Whether the current model runs on run-time specialised kernels (1) or the interpreter (0).
-int psgpu_jit_active(psgpu_ctx* c) { return c && c->jit ? 1 : 0; }
+int psgpu_jit_active(psgpu_ctx* c) {
+    if (!c) return 0;
+    if (c->jitPending && set_device(c) == PSGPU_RET_SUCCESS) jit_poll(c, false);
+    return c->jit ? 1 : 0;
+}
+
+int psgpu_jit_pending(psgpu_ctx* c) {
+    if (!c) return 0;
+    if (c->jitPending && set_device(c) == PSGPU_RET_SUCCESS) jit_poll(c, false);
+    return c->jitPending ? 1 : 0;
+}
+
+int psgpu_jit_wait(psgpu_ctx* c) {
+    if (!c) return 0;
+    if (c->jitPending && set_device(c) == PSGPU_RET_SUCCESS) jit_poll(c, true);
+    return c->jit ? 1 : 0;
+}
 
 // Generated specialised source for the current model (NUL-terminated, truncated to cap).
 int psgpu_jit_source(psgpu_ctx* c, char* buf, size_t cap) {

@@ -2,8 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <future>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "psgpu_model.h"
 
@@ -14,9 +16,23 @@ struct JitKernels {
     hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, finish = nullptr, probe = nullptr;
 };
 
-// Compiled (cached per structure and device) kernels for the model; nullptr + *err on failure.
+extern const char* const kJitArch;  // "gfx950"
+
+// A compiled code object (or the compiler's error) for one generated source.
+struct JitCode {
+    std::string key;         // source + embedded headers + tuning + toolchain
+    std::vector<char> code;  // empty on failure
+    std::string error;
+};
+using JitFuture = std::shared_future<std::shared_ptr<const JitCode>>;
+
+// Request the model's specialised kernels: hiprtc compiles on a host thread (one job per
+// distinct source; an on-disk cache serves repeats unless useDisk is false).  No GPU needed.
 // baked: primitive / op parameters compiled in as literals (recompiles when they change).
-std::shared_ptr<JitKernels> jit_get(const DevModel& m, bool baked, int device, std::string* err);
+JitFuture jit_request(const DevModel& m, bool baked, bool useDisk = true);
+// Load a finished code object on `device` (the calling thread's current device), cached
+// per device; nullptr + *err on failure (a stale cached object is dropped from the cache).
+std::shared_ptr<JitKernels> jit_load(const JitCode& code, int device, std::string* err);
 // Compile (and cache) without loading: code-object size, or -1 and *err.  No GPU needed.
 long jit_compile_only(const DevModel& m, bool baked, std::string* err);
 // The generated HIP source (tests and debugging).

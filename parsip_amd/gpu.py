@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_set_model", "psgpu_polygonize", "psgpu_finish", "psgpu_mesh_device", "psgpu_download_mesh",
     "psgpu_download_stats", "psgpu_export_polympus", "psgpu_polygonize_mpus", "psgpu_last_kernel_times",
     "psgpu_field_values", "psgpu_set_option", "psgpu_jit_active", "psgpu_jit_source", "psgpu_jit_compile",
+    "psgpu_jit_pending", "psgpu_jit_wait",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -55,6 +56,7 @@ OPT_FINISH_BLOCKS_PER_CU = 5
 OPT_CAPACITY = 6
 OPT_GRAPH = 7
 OPT_BOUND = 10
+OPT_JIT_ASYNC = 11
 
 
 def load(build_if_missing: bool = True):
@@ -89,6 +91,8 @@ def load(build_if_missing: bool = True):
         "psgpu_field_values": ([vp, vp, u32, i32, vp, vp], i32),
         "psgpu_set_option": ([vp, i32, ctypes.c_int64], i32),
         "psgpu_jit_active": ([vp], i32),
+        "psgpu_jit_pending": ([vp], i32),
+        "psgpu_jit_wait": ([vp], i32),
         "psgpu_jit_source": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "psgpu_jit_compile": ([vp, vp, vp, i32, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
     }
@@ -197,10 +201,23 @@ class Polygonizer:
         self._L.psgpu_jit_source(self._ctx, buf, n + 1)
         return buf.value.decode()
 
-    def set_model(self, model: soa.Model) -> None:
+    @property
+    def jit_pending(self) -> bool:
+        return bool(self._L.psgpu_jit_pending(self._ctx))
+
+    def jit_wait(self) -> bool:
+        """Block until the model's specialised kernels are compiled; True if they run."""
+        return bool(self._L.psgpu_jit_wait(self._ctx))
+
+    def set_model(self, model: soa.Model, wait_jit: bool = True) -> None:
+        """Upload a model.  The library compiles its specialised kernels on a host thread
+        and serves polygonizations from the interpreter meanwhile (bit-identical output);
+        ``wait_jit`` blocks until they are in place."""
         p, m, o = model.ptrs()
         _check(self._L.psgpu_set_model(self._ctx, p, m, o), "psgpu_set_model")
         self.model = model
+        if wait_jit:
+            self.jit_wait()
 
     def polygonize(self, cellsize: float, mpu_begin: int = 0, mpu_end: int | None = None,
                    stream: int | None = None) -> None:

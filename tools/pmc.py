@@ -1,0 +1,41 @@
+"""Per-kernel PMC summary (per launch, averaged) from the passes of tools/pmc.sh, with
+derived issue figures: VALU issue utilisation at 2 cycles per wave64 VALU instruction
+(CDNA4 SIMD-32, MI355X_MICROARCH.md "Wave scheduling"), waves per SIMD, stall shares.
+Usage: python tools/pmc.py gpurun_out/<tag>  -> JSON on stdout."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d = sys.argv[1]
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for p in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(p)):
+        acc[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+dur = collections.defaultdict(list)
+for p in glob.glob(os.path.join(d, "p*", "**", "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(p)):
+        dur[r["Kernel_Name"].split("(")[0]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+out = {"note": "per launch; valu_issue = SQ_INSTS_VALU x 2 cyc / (us x 2400 x 1024 SIMDs); SQ_*_CYCLES and "
+               "SQ_WAIT_* count quad-cycles (MI355X_MICROARCH.md); profiled clocks run lower than un-profiled",
+       "kernels": {}}
+for k, c in acc.items():
+    if "rocclr" in k or "__amd" in k:
+        continue
+    e = {n: sum(v) / len(v) for n, v in c.items()}
+    if dur.get(k):
+        us = sorted(dur[k])[len(dur[k]) // 2]
+        e["median_us_profiled"] = us
+        if "SQ_INSTS_VALU" in e:
+            e["valu_issue"] = round(e["SQ_INSTS_VALU"] * 2 / (us * 2400 * 1024), 4)
+    wc = e.get("SQ_WAVE_CYCLES")
+    if wc:
+        for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if n in e:
+                e["share_" + n[3:].lower()] = round(e[n] / wc, 3)
+    if e.get("SQ_WAVES") and wc:
+        e["quad_cycles_per_wave"] = round(wc / e["SQ_WAVES"], 1)
+    out["kernels"][k] = e
+print(json.dumps(out, indent=1))
