@@ -2,15 +2,19 @@
 """Benchmark: Mcells/s polygonized, 256^3 grid, 32-primitive BlobTree (BASELINE.json).
 
 One step = one full polygonization of the C3 workload (32 prims, 31 ops
-with Union/Dif, 256^3 cells over [-4,4]^3 = 50,653 MPUs) on one GPU with the model
-already resident in HBM: S1 precheck -> compaction -> per-MPU field cache, classification
-and vertex ownership -> offsets -> vertices (root, colour, normal) -> triangles.  The
-compact mesh stays in HBM.
+with Union/Dif, 256^3 cells over [-4,4]^3 = 50,653 MPUs) with the model already resident
+in HBM: S1 precheck -> compaction -> per-MPU field cache, classification and vertex
+ownership -> offsets -> vertices (root, colour, normal) -> triangles.  The compact mesh
+stays in HBM.
 
-N GPUs (torchrun, one process per GPU): weak scaling.  Rank r polygonizes its own
-256^3 grid of frame r of the animated C3 tree (independent objects, no data-path
-collective); value = N * 256^3 / max-over-ranks step time.  `--scaling strong` instead
-splits one 256^3 grid into contiguous MPU ranges (config C4).
+N GPUs (one process per GPU: under torch.distributed.run, or `--gpus N` alone, which
+spawns the N ranks itself before any HIP call): strong scaling by default, config C4 —
+ONE 256^3 grid split into N contiguous MPU ranges of near-equal cost (the split comes
+from one full planning run on every rank, deterministic, so all ranks agree without
+communication); every step each rank polygonizes its range and the ranks exchange their
+(MPUs, V, T, ...) totals with one RCCL all-gather on the library's stream (the only
+collective: MPUs are independent, no halo).  value = 256^3 / max-over-ranks step time.
+`--scaling weak` instead gives every rank its own grid (frame r of the animated tree).
 
 Output: one JSON line on rank 0 (the driver's contract) with `roofline` for the dominant
 kernel (hipEvent-timed on the library's stream) and `cpu_baseline` (the oracle, rank 0,
@@ -19,8 +23,10 @@ N=1 only).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -29,15 +35,34 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from parsip_amd import costmodel, gpu, synth  # noqa: E402
+from parsip_amd import costmodel, gpu, synth  # noqa: E402  (no HIP call at import)
 
-VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)" (= FP32 MFMA rate)
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)": 256 CU x 4 SIMD-32 x 2.4 GHz x 64 (FMA)
 HBM_PEAK_GBS = 8000.0
+METRIC = "Mcells/sec polygonized, 256^3 grid 32-prim BlobTree, at 1/2/4/8 MI355X"
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside a launcher: start N rank processes (one per GPU) as
+    children before this process touches a GPU, wait, return the worst exit code."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
 
 
 class Group:
-    """Barrier / max-reduce across ranks.  torch.distributed (gloo, CPU tensors) is only
-    imported for N > 1 and after the HIP library has initialised the device."""
+    """Barrier / max-reduce / broadcast across ranks over gloo (CPU).  torch.distributed is
+    imported only for N > 1 and after the HIP library has initialised the device (the
+    library's ROCm runtime is then the one loaded in the process)."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,6 +91,11 @@ class Group:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def broadcast_bytes(self, b: bytes | None) -> bytes:
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
     def allgather(self, vals):
         if not self.dist:
             return [list(vals)]
@@ -77,23 +107,24 @@ class Group:
         return [o.tolist() for o in out]
 
 
-def measured_traffic(kernel: str, jit: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/<round>_traffic.json, made by tools/gpu_round.sh + tools/traffic.py on the
-    same workload): 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE.  None if absent."""
-    import glob
-
-    names = [f"jit_{kernel[2:]}" if jit else f"psgpu::{kernel}", kernel]
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+def committed_profile(kind: str):
+    """Newest committed rocprofv3 summary of `kind` (profiles/rNN*_<kind>.json)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{kind}.json")), reverse=True):
         try:
             with open(path) as f:
-                ks = json.load(f)["kernels"]
+                return json.load(f)["kernels"], os.path.relpath(path, ROOT)
         except (OSError, ValueError, KeyError):
             continue
-        for n in names:
-            if n in ks and "traffic_bytes" in ks[n]:
-                return ks[n]["traffic_bytes"], os.path.basename(path)
     return None, None
+
+
+def profile_entry(kernels, kernel: str, jit: int):
+    if not kernels:
+        return None
+    for n in ([f"jit_{kernel[2:]}"] if jit else []) + [f"psgpu::{kernel}", kernel]:
+        if n in kernels:
+            return kernels[n]
+    return None
 
 
 def workload_ops(config: str):
@@ -105,27 +136,25 @@ def workload_ops(config: str):
         return None
 
 
-def valu_utilisation(kernel: str, jit: int, ms: float):
-    """VALU issue utilisation of `kernel` from the committed PMC pass
-    (profiles/*_valu.json: SQ_INSTS_VALU per launch): instructions x 4 cycles (wave64 on
-    16-lane SIMDs) over the launch's SIMD-cycles (1024 SIMDs at 2.4 GHz)."""
-    import glob
-
-    names = [f"jit_{kernel[2:]}" if jit else f"psgpu::{kernel}", kernel]
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), reverse=True):
-        try:
-            with open(path) as f:
-                ks = json.load(f)["kernels"]
-        except (OSError, ValueError, KeyError):
-            continue
-        for n in names:
-            if n in ks and "SQ_INSTS_VALU" in ks[n]:
-                return round(ks[n]["SQ_INSTS_VALU"] * 4 / (ms * 1e-3 * 2.4e9 * 1024), 4), os.path.basename(path)
-    return None, None
+def cpu_info():
+    model, smt = "unknown", None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        smt = open("/sys/devices/system/cpu/smt/active").read().strip() == "1"
+    except OSError:
+        pass
+    return model, smt
 
 
 def cpu_baseline(model, cs, n_cells):
-    """The oracle (CPU restatement, 'port') on the host's cores: bounded sample."""
+    """The oracle (oracle/psoracle.c, the CPU restatement of the reference: "port") on the
+    host's cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import psoracle
 
@@ -141,18 +170,22 @@ def cpu_baseline(model, cs, n_cells):
         psoracle.polygonize(model, cs, threads=threads, keep=False)
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
+    cpu_model, smt = cpu_info()
     return {"value": round(n_cells / med / 1e6, 3), "unit": "Mcells/s", "cores": threads, "kind": "port",
             "sample": f"full C3 256^3 polygonization x{len(times)} (median {med * 1e3:.1f} ms, "
-                      f"best {min(times) * 1e3:.1f} ms), oracle/psoracle.c with {threads} threads"}
+                      f"best {min(times) * 1e3:.1f} ms) by oracle/psoracle.c, the plain-C restatement of the "
+                      f"reference (PS_Polygonizer.cpp; the reference binary is not built here), {threads} threads",
+            "cpu_model": cpu_model, "nproc": os.cpu_count(), "smt_active": smt}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="N>1: strong (default: one grid split over the ranks) or weak (a grid per rank)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
@@ -160,10 +193,18 @@ def main():
     ap.add_argument("--debug", type=int, default=0, help=argparse.SUPPRESS)  # profiling ablations only
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     grp = Group()
+    if grp.world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={grp.world}: launch one process per GPU")
+    scaling = args.scaling or ("strong" if grp.world > 1 else "weak")
+
     # one process per GPU (LOCAL_RANK); PSGPU_BENCH_DEVICE pins every rank to one device
-    # (multi-rank rehearsal on a one-GPU box)
-    poly = gpu.Polygonizer(int(os.environ.get("PSGPU_BENCH_DEVICE", grp.local)))  # HIP before torch
+    # (multi-rank rehearsal on a one-GPU box: the count exchange then runs over gloo)
+    pinned = os.environ.get("PSGPU_BENCH_DEVICE")
+    device = int(pinned) if pinned is not None else grp.local
+    poly = gpu.Polygonizer(device)  # HIP before torch
     grp.init()
     if args.no_cull:
         poly.set_option(gpu.OPT_CULLING, 0)
@@ -171,60 +212,114 @@ def main():
     if args.debug:
         poly.set_option(gpu.OPT_DEBUG, args.debug)
 
-    frame = grp.rank if args.scaling == "weak" else 0
+    frame = grp.rank if scaling == "weak" else 0
     model, cs, N = synth.make_config(args.config, frame=frame)
-    t_model = time.perf_counter()
-    poly.set_model(model)  # uploads the SoA and builds/compiles the tree kernels
-    t_model = time.perf_counter() - t_model
+    t0 = time.perf_counter()
+    poly.set_model(model, wait_jit=False)  # uploads the SoA; hiprtc compiles on a host thread
+    t_model = time.perf_counter() - t0
+    jit_on = poly.jit_wait() if args.jit else False
+    t_jit = time.perf_counter() - t0
     n_mpus = gpu.count_mpus(cs, *model.bbox)
-    if args.scaling == "strong" and grp.world > 1:
-        per = (n_mpus + grp.world - 1) // grp.world
-        begin, end = grp.rank * per, min(n_mpus, (grp.rank + 1) * per)
+
+    comm, exchange = None, None
+    full = None
+    if scaling == "strong" and grp.world > 1:
+        bounds = poly.plan_split(cs, grp.world)  # one full run; the same split on every rank
+        full = poly.finish()
+        begin, end = int(bounds[grp.rank]), int(bounds[grp.rank + 1])
+        if pinned is None:
+            uid = grp.broadcast_bytes(gpu.comm_unique_id() if grp.rank == 0 else None)
+            comm = gpu.Comm(poly, uid, grp.world, grp.rank)
+            exchange = "rccl all-gather of 8 words per rank per step (library stream)"
+        else:
+            exchange = "gloo all-gather after the timed steps (ranks share one device: RCCL needs distinct GPUs)"
     else:
         begin, end = 0, n_mpus
 
+    def step():
+        poly.polygonize(cs, begin, end)
+        if comm:
+            comm.exchange()
+
+    def finish():
+        if comm:
+            return comm.result()
+        return poly.finish(), None
+
     for _ in range(args.warmup):
-        poly.run(cs, begin, end)
+        step()
+        finish()
     grp.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        poly.polygonize(cs, begin, end)
-    info = poly.finish()
+        step()
+    info, parts = finish()
     grp.barrier()
     t1 = time.perf_counter()
     dt = grp.max(t1 - t0)
     ms_step = dt / args.steps * 1e3
-    cells_per_step = N ** 3 * (grp.world if args.scaling == "weak" else 1)
+    cells_per_step = N ** 3 * (grp.world if scaling == "weak" else 1)
     value = cells_per_step / (ms_step * 1e-3) / 1e6
 
+    mine = poly.finish()
+    counts = grp.allgather([mine.ctMPUs, mine.ctVertices, mine.ctTriangles])
+    check = None
+    if full is not None:  # the parts must add up to the full grid of the planning run
+        tot = [sum(c[i] for c in counts) for i in range(3)]
+        ok = tot == [full.ctMPUs, full.ctVertices, full.ctTriangles]
+        if comm:
+            ok = ok and (info.ctMPUs, info.ctVertices, info.ctTriangles) == tuple(tot)
+        check = {"parts_sum_to_full_grid": ok, "full": [full.ctMPUs, full.ctVertices, full.ctTriangles]}
+        if not ok:
+            sys.exit(f"bench.py rank {grp.rank}: parts {counts} do not add up to the full grid {check['full']}")
+
     # roofline pass: per-kernel hipEvent timing on the library's stream
-    poly.set_option(1, 1)
+    poly.set_option(gpu.OPT_KERNEL_TIMING, 1)
     kt = {}
-    reps = max(3, min(args.steps, 10))
+    reps = max(3, min(args.steps, 20))
     for _ in range(reps):
         poly.run(cs, begin, end)
         for k, v in poly.kernel_times().items():
             kt[k] = kt.get(k, 0.0) + v / reps
-    poly.set_option(1, 0)
+    poly.set_option(gpu.OPT_KERNEL_TIMING, 0)
     dom = max(kt, key=kt.get)
-    per_eval = costmodel.ops_per_eval(model)
-    kernel_evals = {"k_precheck": 8 * info.ctMPUs, "k_mpu": 512 * info.ctPassedPrecheck,
-                    "k_vertex": 7 * info.ctVertices, "k_finish": info.ctVertices}
-    # algorithmic work: the fp32 ops the reference executes on this input (after its own
-    # op-box pruning), counted by the oracle and priced by costmodel
-    # (tests/golden/workload_ops.json); else SURVEY §8(d)'s unpruned per-eval figure
-    wops = workload_ops(args.config)
-    if wops and wops.get("vertices") == info.ctVertices and dom in wops:
-        dom_flops, flops_src = wops[dom], "tests/golden/workload_ops.json (reference-executed ops)"
-    else:
-        dom_flops, flops_src = kernel_evals.get(dom, 0) * per_eval, "lane-evals x costmodel.ops_per_eval"
-    achieved = dom_flops / (kt[dom] * 1e-3) / 1e12
-    counts = grp.allgather([info.ctVertices, info.ctTriangles])
-    traffic, traffic_src = measured_traffic(dom, args.jit) if args.config == "C3" else (None, None)
-    valu_util, valu_src = valu_utilisation(dom, args.jit, kt[dom]) if args.config == "C3" else (None, None)
+    # lane-evaluations each launch processes (SURVEY.md §8(d) units) ...
+    launch_evals = {"k_precheck": 8 * mine.ctMPUs, "k_mpu": 512 * mine.ctFieldMPUs,
+                    "k_vertex": 4 * mine.ctVertices, "k_finish": 4 * mine.ctVertices}
+    # ... times the fp32 ops per lane-evaluation of that stage that the reference executes on
+    # this input (its own op-box pruning included; the oracle's counters priced by
+    # parsip_amd/costmodel.py, tests/golden/workload_ops.json); else the unpruned figure
+    wops = workload_ops(args.config) if scaling == "weak" or grp.world == 1 else None
+    per_eval, per_src = costmodel.ops_per_eval(model), "costmodel.ops_per_eval (unpruned tree)"
+    if wops and wops.get("vertices") == mine.ctVertices and dom in wops:
+        ref_evals = {"k_precheck": 8 * mine.ctMPUs, "k_mpu": 512 * wops["passed_s1"],
+                     "k_vertex": 4 * wops["vertices"], "k_finish": 4 * wops["vertices"]}[dom]
+        per_eval, per_src = wops[dom] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
+    alg_ops = launch_evals[dom] * per_eval
+    achieved = alg_ops / (kt[dom] * 1e-3) / 1e12
+    pmc, pmc_src = committed_profile("pmc")
+    pe = profile_entry(pmc, dom, args.jit) if args.config == "C3" and grp.world == 1 else None
+    tr, tr_src = committed_profile("traffic")
+    te = profile_entry(tr, dom, args.jit) if args.config == "C3" and grp.world == 1 else None
+    roof = {"bound": "valu", "pipe": "fp32 VALU (no MFMA: scalar field evaluation; SURVEY.md §8(d))",
+            "kernel": dom, "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
+            "traffic": round(te["traffic_bytes"]) if te and "traffic_bytes" in te else None,
+            "traffic_source": tr_src if te else None,
+            "kernel_ms": round(kt[dom], 4), "lane_evals": launch_evals[dom], "ops_per_eval": round(per_eval, 1),
+            "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
+            "note": "achieved = lane-evaluations this launch performs x the reference's fp32 ops per "
+                    "evaluation / hipEvent launch time; exact per-wave culling skips part of those ops, so "
+                    "valu_issue (executed VALU instructions x 2 cycles per wave64 on SIMD-32, PMC) is the "
+                    "hardware-side utilisation"}
+    if pe and "SQ_INSTS_VALU" in pe:
+        roof["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (kt[dom] * 1e-3 * 2.4e9 * 1024), 4)
+        roof["valu_source"] = pmc_src
+    if te and "avg_us" in te:
+        roof["rocprof_avg_us"] = te["avg_us"]
 
     out = {
-        "metric": "Mcells/sec polygonized, 256^3 grid 32-prim BlobTree, at 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "Mcells/s",
         "n_gpus": grp.world,
@@ -232,36 +327,34 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: C3 BlobTree from std::mt19937(42) as in the reference probe (SURVEY.md §6, §8(d))",
-        "config": {"workload": f"{args.config}: {model.ct_prims}-prim/{model.ct_ops}-op BlobTree, {N}^3 cells, "
-                               f"{n_mpus} MPUs" + (f", frame=rank" if args.scaling == "weak" and grp.world > 1 else ""),
+        "config": {"workload": (f"{args.config}: {model.ct_prims}-prim/{model.ct_ops}-op BlobTree, {N}^3 cells, "
+                                f"{n_mpus} MPUs")
+                               + (" split over the ranks (C4)" if full is not None else "")
+                               + (", a grid per rank (frame = rank)" if scaling == "weak" and grp.world > 1 else ""),
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,
-                   "parallelism": f"{args.scaling}-{grp.world}gpu",
-                   "mpu_range": [begin, end], "culling": not args.no_cull,
-                   "kernels": ["interpreter", "jit-structure", "jit-baked"][args.jit] if poly.jit_active or args.jit == 0
-                   else "interpreter (jit unavailable)", "set_model_s": round(t_model, 3)},
-        "roofline": {"bound": "mfma", "pipe": "fp32 VALU (peak = FP32 vector = FP32 MFMA rate)",
-                     "kernel": dom, "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
-                     "traffic": None if traffic is None else round(traffic),
-                     "traffic_source": traffic_src,
-                     "kernel_ms": round(kt[dom], 4), "algorithmic_ops": dom_flops, "ops_source": flops_src,
-                     "note": "exact culling skips ~90% of the primitive evaluations the reference executes, so "
-                             "reference-equivalent throughput can reach the VALU peak; valu_issue_util is the "
-                             "hardware-side figure",
-                     "valu_issue_util": valu_util, "valu_source": valu_src},
+                   "parallelism": f"{scaling}-{grp.world}gpu", "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
+                   "exchange": exchange, "culling": not args.no_cull,
+                   "kernels": ["interpreter", "jit-structure", "jit-baked"][args.jit] if jit_on or args.jit == 0
+                   else "interpreter (jit unavailable)", "set_model_s": round(t_model, 4),
+                   "jit_ready_s": round(t_jit, 3)},
+        "roofline": roof,
         "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
         "mesh": {"vertices": info.ctVertices, "triangles": info.ctTriangles, "passed_s1": info.ctPassedPrecheck,
                  "surface_mpus": info.ctSurfaceMPUs, "field_mpus": info.ctFieldMPUs, "per_rank": counts},
-        "hbm_gbs_algorithmic": round((info.ctVertices * 36 + info.ctTriangles * 12) / (ms_step * 1e-3) / 1e9, 2),
+        "hbm_gbs_algorithmic": round((mine.ctVertices * 36 + mine.ctTriangles * 12) / (ms_step * 1e-3) / 1e9, 2),
     }
+    if check:
+        out["check"] = check
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3)
     if grp.rank == 0:
         print(json.dumps(out), flush=True)
+    if comm:
+        comm.close()
     if grp.dist:
         grp.dist.destroy_process_group()
     poly.close()

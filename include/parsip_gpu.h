@@ -250,6 +250,85 @@ int  psgpu_jit_wait(psgpu_ctx* ctx);
 /* Generated specialised HIP source of the current model; returns its length. */
 int  psgpu_jit_source(psgpu_ctx* ctx, char* buf, size_t cap);
 
+/* Per-MPU work of the last run in lane-evaluations (8 S1 + 64 field bounds of a survivor
+ * or 512 S2 cache of a queued survivor + 8 per vertex), ctMPUs entries. */
+int  psgpu_mpu_costs(psgpu_ctx* ctx, uint32_t* costs);
+/* Contiguous ranges of near-equal cost over n MPUs starting at global id `begin`:
+ * bounds[0..parts] (bounds[0] = begin, bounds[parts] = begin + n).  Host only. */
+int  psgpu_split_costs(const uint32_t* costs, uint32_t n, uint32_t parts, uint32_t begin,
+                       uint32_t* bounds);
+
+/* ---- one grid over several devices (one process) --------------------------
+ * The reference's Polygonize fans the MPU list over every core in one blocking call
+ * (tbb::parallel_for, PS_Polygonizer.cpp:379-382); a group fans one MPU lattice over
+ * several GPUs: contiguous MPU ranges of near-equal cost, one context per device, every
+ * device launched at once.  Parts concatenated in order are exactly the single-device
+ * mesh (MPUs are independent: no halo).  Several parts may share a device. */
+typedef struct psgpu_group psgpu_group;
+typedef struct PsGroupPart {
+    int32_t  device;          /* HIP ordinal (-1: another rank's device, psgpu_comm)  */
+    uint32_t mpuBegin;        /* global MPU range [mpuBegin, mpuEnd)                  */
+    uint32_t mpuEnd;
+    uint32_t vertexBase;      /* first vertex / triangle of the part in the whole mesh */
+    uint32_t triangleBase;
+    uint32_t reserved;
+    PsMeshInfo info;          /* the part's own counts                                 */
+} PsGroupPart;
+
+#define PSGPU_GROUP_OPT_BALANCE       100 /* range split policy (value below)           */
+#define PSGPU_GROUP_BALANCE_EVEN        0 /* equal MPU counts                            */
+#define PSGPU_GROUP_BALANCE_PLAN        1 /* cost split from a planning run of the whole
+                                             lattice, redone when the lattice changes
+                                             (default)                                  */
+#define PSGPU_GROUP_BALANCE_EVERY_RUN   2 /* plan, then re-split after every finish from
+                                             the costs of that run (animations)          */
+#define PSGPU_GROUP_BALANCE_FIXED       3 /* the split of psgpu_group_set_split          */
+
+/* devices: nParts HIP ordinals (NULL: 0 .. nParts-1). */
+int  psgpu_group_create(const int* devices, int nParts, psgpu_group** out);
+void psgpu_group_destroy(psgpu_group* g);
+int  psgpu_group_size(psgpu_group* g);
+/* The context of one part (its device-resident part of the mesh, options, timing). */
+psgpu_ctx* psgpu_group_context(psgpu_group* g, int part);
+/* PSGPU_GROUP_OPT_BALANCE, or any PSGPU_OPT_* (applied to every part). */
+int  psgpu_group_set_option(psgpu_group* g, int option, int64_t value);
+int  psgpu_group_set_model(psgpu_group* g, const PsSoaBlobPrims* prims,
+                           const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops);
+int  psgpu_group_jit_wait(psgpu_group* g);
+/* Explicit split: bounds[0..nParts] global MPU ids, non-decreasing (policy FIXED). */
+int  psgpu_group_set_split(psgpu_group* g, const uint32_t* bounds);
+int  psgpu_group_get_split(psgpu_group* g, uint32_t* bounds);
+/* Enqueue the whole lattice over the parts (asynchronous on every device). */
+int  psgpu_group_polygonize(psgpu_group* g, float cellsize);
+/* Wait for every part; totals over the parts and, if parts != NULL, nParts entries. */
+int  psgpu_group_finish(psgpu_group* g, PsMeshInfo* total, PsGroupPart* parts);
+/* The whole mesh to host arrays (global vertex ids and MPU offsets, as one device). */
+int  psgpu_group_download_mesh(psgpu_group* g, float* pos, float* nrm, float* col, uint32_t* tris,
+                               uint64_t* mpuOffsets);
+/* The whole mesh in HBM of part dstPart's device (peer copies over xGMI + rebase). */
+int  psgpu_group_gather(psgpu_group* g, int dstPart, PsMeshDevice* out);
+int  psgpu_group_export_polympus(psgpu_group* g, PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs);
+/* Blocking drop-in for PS::SIMDPOLY::Polygonize over every device of the group. */
+int  psgpu_group_polygonize_mpus(psgpu_group* g, float cellsize, const PsSoaBlobPrims* prims,
+                                 const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops,
+                                 PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs);
+
+/* ---- one process per GPU: the count exchange over RCCL (xGMI) --------------
+ * Every rank polygonizes its range of one split (psgpu_split_costs of the same costs on
+ * every rank) on its own context; psgpu_comm_exchange all-gathers each rank's totals
+ * (8 words, written by the run's last kernel) on the context's stream. */
+typedef struct psgpu_comm psgpu_comm;
+#define PSGPU_COMM_ID_BYTES 128
+/* Rank 0 makes the id; the caller broadcasts its bytes to the other ranks. */
+int  psgpu_comm_unique_id(uint8_t id[PSGPU_COMM_ID_BYTES]);
+int  psgpu_comm_create(psgpu_ctx* ctx, const uint8_t id[PSGPU_COMM_ID_BYTES], int nranks, int rank,
+                       psgpu_comm** out);
+void psgpu_comm_destroy(psgpu_comm* comm);
+/* Enqueue the all-gather of the context's last polygonization (after psgpu_polygonize). */
+int  psgpu_comm_exchange(psgpu_comm* comm, psgpu_ctx* ctx);
+/* Wait; totals over all ranks and, if parts != NULL, nranks entries (rank order). */
+int  psgpu_comm_result(psgpu_comm* comm, PsMeshInfo* total, PsGroupPart* parts);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -674,7 +674,8 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const bool vOf = __shfl(valid ? 1 : 0, lane * 8 & 63) != 0;
     const bool pass = lane < 8 && ((queue8 >> lane) & 1u);
     if (lane < 8 && vOf) {
-        p.passed[mOf - p.mpuBegin] = (uint8_t)((flags8 >> lane) & 1u);
+        // 0: failed S1; 1: passed, proven empty by field bounds; 2: passed, queued for S2
+        p.passed[mOf - p.mpuBegin] = (uint8_t)(((flags8 >> lane) & 1u) + ((queue8 >> lane) & 1u));
         if (!pass) p.counts[mOf - p.mpuBegin] = 0ull;
     }
     if (flags8 == 0u) return;
@@ -1258,6 +1259,16 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
         for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
         for (uint32_t i = threadIdx.x; i < kScanMaxBlocks; i += blockDim.x) p.scanStatusNext[i] = 0ull;
+        if (threadIdx.x < 64) {  // the run's totals for the count exchange between parts (RCCL)
+            const ShardCtr& sc = p.ctr->shard[threadIdx.x];
+            const uint32_t tv = wave_sum(sc.v), tt = wave_sum(sc.t), tp = wave_sum(sc.p), tb = wave_sum(sc.b),
+                           ts = wave_sum(sc.s);
+            if (threadIdx.x == 0) {
+                const uint32_t tot[8] = {p.mpuCount, tv, tt, tp + tb, ts, tp, (uint32_t)p.ctr->firstOverflow,
+                                         p.ctr->error};
+                for (int i = 0; i < 8; ++i) p.totals[i] = tot[i];
+            }
+        }
     }
     const ShardBatches sv(&p.ctr->shard[0].v, p.vShardCap, 64);
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {

@@ -19,9 +19,8 @@
 #include <vector>
 
 #include "../../include/parsip_gpu.h"
-#include "psgpu_jit.h"
+#include "psgpu_internal.h"
 #include "psgpu_launch.h"
-#include "psgpu_model.h"
 
 using namespace psgpu;
 
@@ -371,90 +370,21 @@ hipError_t grow(T*& ptr, size_t& cap, size_t need) {
     return e;
 }
 
-constexpr int kNumKernels = 4;
 const char* kKernelNames[kNumKernels] = {"k_precheck", "k_mpu", "k_vertex", "k_finish"};
 
 }  // namespace
 
-struct psgpu_ctx {
-    int device = 0;
-    int numCUs = 256;
-    hipStream_t stream = nullptr;
-    PsSoaBlobPrims primsHost;  // bbox + counts of the current model
-    DevModel model{};
-    DevModel* dModel = nullptr;
-    CubeTablesDev* dTables = nullptr;
-    int useJit = 1;
-    int jitAsync = 1;                  // set_model returns while hiprtc compiles (interpreter meanwhile)
-    std::shared_ptr<JitKernels> jit;   // specialised kernels of the current model
-    JitFuture jitFut;                  // the current model's compile, while jitPending
-    bool jitPending = false;
-    std::string jitError;
-    bool haveModel = false;
-    int cull = 1;
-    int debug = 0;
-    int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
-    int finishBlocksPerCU = 8;
-    int timing = 0;
-    // geometry of the last run
-    float cs = 0.0f;
-    uint32_t dims[3] = {0, 0, 0};
-    uint32_t mpuBegin = 0, mpuCount = 0;
-    hipStream_t runStream = nullptr;
-    bool pending = false;
-    bool haveResult = false;
-    // device buffers
-    size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
-    uint32_t* pq = nullptr;         // sharded S1 survivor queues
-    uint32_t pShardCap = 0;
-    uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
-    uint32_t parity = 0;            // which counter / status set the next run uses
-    uint64_t* counts = nullptr;
-    uint8_t* passed = nullptr;      // per MPU: passed S1
-    size_t capPassed = 0;
-    int bound = 1;                  // prove S1 survivors empty by field bounds in k_precheck
-    uint64_t* mpuMasks = nullptr;
-    size_t capMasks = 0;
-    uint64_t* offs = nullptr;
-    VertexRec* vq = nullptr;
-    TriRec* tq = nullptr;
-    float* pos = nullptr;
-    float* nrm = nullptr;
-    float* col = nullptr;
-    uint32_t* tris = nullptr;
-    DevCounters* ctr = nullptr;         // two sets, alternating runs
-    DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
-    DevCounters* hostCtrDev = nullptr;  // its device address
-    uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
-    uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
-    hipEvent_t ev[kNumKernels + 1] = {};
-    int useGraph = 0;  // replay repeated launch sequences from a hipGraph (measured slower on ROCm 7.2)
-    struct GraphSlot {
-        hipGraphExec_t exec = nullptr;
-        JitKernels* jit = nullptr;
-        Params key{};
-        uint32_t shape[3] = {0, 0, 0};
-    } graphs[2];
-    float lastMs[kNumKernels] = {};
-    PsMeshInfo info{};
-    // high-water marks of finished runs: the next run's buffers are sized from them
-    // (an animation whose mesh grows frame to frame does not pay a synchronous re-run)
-    uint32_t seenV = 0, seenT = 0, seenShardV = 0, seenShardT = 0;
-};
-
-namespace {
-
+namespace psgpu {
 int hip_fail(hipError_t e, const char* what) {
     if (e == hipSuccess) return PSGPU_RET_SUCCESS;
     fprintf(stderr, "psgpu: %s failed: %s\n", what, hipGetErrorString(e));
     return e == hipErrorOutOfMemory ? PSGPU_RET_NOT_ENOUGH_MEM : PSGPU_RET_DEVICE_ERROR;
 }
 
-#define PSGPU_CHECK(expr)                                   \
-    do {                                                    \
-        hipError_t _e = (expr);                             \
-        if (_e != hipSuccess) return hip_fail(_e, #expr);   \
-    } while (0)
+int set_device(psgpu_ctx* c) { return hip_fail(hipSetDevice(c->device), "hipSetDevice"); }
+}  // namespace psgpu
+
+namespace {
 
 // k_precheck covers the MPU range with 2x2x2 bricks of MPUs (one per wavefront: a
 // compact box for its culling test), whole brick rows along x.
@@ -532,6 +462,7 @@ Params make_params(psgpu_ctx* c) {
     p.ctr = c->ctr + c->parity;
     p.ctrNext = c->ctr + (c->parity ^ 1u);
     p.hostCtr = c->hostCtrDev;
+    p.totals = c->totals;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     p.debug = (uint32_t)c->debug;
     return p;
@@ -621,8 +552,6 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     PSGPU_CHECK(hipGraphLaunch(g.exec, s));
     return PSGPU_RET_SUCCESS;
 }
-
-int set_device(psgpu_ctx* c) { return hip_fail(hipSetDevice(c->device), "hipSetDevice"); }
 
 // Adopt the model's specialised kernels once their compile has finished (wait: block for
 // it).  Until then the interpreter runs; its output is bit-identical.  Call with the
@@ -847,6 +776,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
         hipMemcpy(c->dTables, &tabHost, sizeof(CubeTablesDev), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&c->dModel, sizeof(DevModel)) != hipSuccess ||
         hipMalloc(&c->ctr, 2 * sizeof(DevCounters)) != hipSuccess ||
+        hipMalloc(&c->totals, 8 * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->scanStatus, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(c->scanStatus, 0, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&c->hostCtr, sizeof(DevCounters), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -881,7 +811,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     drop_graphs(c);
     c->jit.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
-                    c->pos, c->nrm, c->col, c->tris, c->ctr};
+                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hostCtr) (void)hipHostFree(c->hostCtr);
@@ -1124,6 +1054,43 @@ int psgpu_download_stats(psgpu_ctx* c, PsMpuStats* stats) {
     }
     return PSGPU_RET_SUCCESS;
 }
+// Per-MPU work of the last run in lane-evaluations: 8 (S1) + 64 (field
+// bounds of a survivor) or 512 (S2 cache of a queued survivor) + 8 per vertex (4 root
+// samples, value and 3 normal samples).  Balances MPU ranges across devices.
+int psgpu_mpu_costs(psgpu_ctx* c, uint32_t* costs) {
+    PsMeshInfo I;
+    int rc = psgpu_finish(c, &I);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (!costs) return PSGPU_RET_PARAM_ERROR;
+    const uint32_t n = c->mpuCount;
+    if (!n) return PSGPU_RET_SUCCESS;
+    std::vector<uint8_t> passed(n);
+    std::vector<uint64_t> cnt(n);
+    PSGPU_CHECK(hipMemcpy(passed.data(), c->passed, n, hipMemcpyDeviceToHost));
+    PSGPU_CHECK(hipMemcpy(cnt.data(), c->counts, (size_t)n * 8, hipMemcpyDeviceToHost));
+    for (uint32_t l = 0; l < n; ++l)
+        costs[l] = 8u + (passed[l] == 1 ? 64u : 0u) + (passed[l] == 2 ? 512u : 0u) + 8u * (uint32_t)cnt[l];
+    return PSGPU_RET_SUCCESS;
+}
+
+// Contiguous ranges of near-equal cost: bounds[k] = begin + the first index whose cost
+// prefix reaches k/parts of the total (bounds[0] = begin, bounds[parts] = begin + n).
+int psgpu_split_costs(const uint32_t* costs, uint32_t n, uint32_t parts, uint32_t begin, uint32_t* bounds) {
+    if (!bounds || parts == 0 || (n && !costs)) return PSGPU_RET_PARAM_ERROR;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += costs[i];
+    bounds[0] = begin;
+    uint64_t acc = 0;
+    uint32_t i = 0;
+    for (uint32_t k = 1; k < parts; ++k) {
+        const uint64_t target = (total * k + parts / 2) / parts;
+        while (i < n && acc + costs[i] / 2 < target) acc += costs[i++];
+        bounds[k] = begin + i;
+    }
+    bounds[parts] = begin + n;
+    return PSGPU_RET_SUCCESS;
+}
+
 int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt) {
     PsMeshInfo I;
     int rc = psgpu_finish(c, &I);

@@ -1,0 +1,106 @@
+// psgpu_internal.h — the device context shared by the library's host sources
+// (psgpu_host.cpp: one context, psgpu_group.cpp: contexts over several devices and the
+// multi-process count exchange).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+
+#include "../../include/parsip_gpu.h"
+#include "psgpu_jit.h"
+#include "psgpu_model.h"
+
+namespace psgpu {
+constexpr int kNumKernels = 4;
+}  // namespace psgpu
+
+struct psgpu_ctx {
+    using JitKernels = psgpu::JitKernels;
+    using JitFuture = psgpu::JitFuture;
+    using DevModel = psgpu::DevModel;
+    using Params = psgpu::Params;
+    using DevCounters = psgpu::DevCounters;
+    using VertexRec = psgpu::VertexRec;
+    using TriRec = psgpu::TriRec;
+    using CubeTablesDev = psgpu::CubeTablesDev;
+    static constexpr int kNumKernels = psgpu::kNumKernels;
+    int device = 0;
+    int numCUs = 256;
+    hipStream_t stream = nullptr;
+    PsSoaBlobPrims primsHost;  // bbox + counts of the current model
+    DevModel model{};
+    DevModel* dModel = nullptr;
+    CubeTablesDev* dTables = nullptr;
+    int useJit = 1;
+    int jitAsync = 1;                  // set_model returns while hiprtc compiles (interpreter meanwhile)
+    std::shared_ptr<JitKernels> jit;   // specialised kernels of the current model
+    JitFuture jitFut;                  // the current model's compile, while jitPending
+    bool jitPending = false;
+    std::string jitError;
+    bool haveModel = false;
+    int cull = 1;
+    int debug = 0;
+    int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
+    int finishBlocksPerCU = 8;
+    int timing = 0;
+    // geometry of the last run
+    float cs = 0.0f;
+    uint32_t dims[3] = {0, 0, 0};
+    uint32_t mpuBegin = 0, mpuCount = 0;
+    hipStream_t runStream = nullptr;
+    bool pending = false;
+    bool haveResult = false;
+    // device buffers
+    size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
+    uint32_t* pq = nullptr;         // sharded S1 survivor queues
+    uint32_t pShardCap = 0;
+    uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
+    uint32_t parity = 0;            // which counter / status set the next run uses
+    uint64_t* counts = nullptr;
+    uint8_t* passed = nullptr;      // per MPU: passed S1
+    size_t capPassed = 0;
+    int bound = 1;                  // prove S1 survivors empty by field bounds in k_precheck
+    uint64_t* mpuMasks = nullptr;
+    size_t capMasks = 0;
+    uint64_t* offs = nullptr;
+    VertexRec* vq = nullptr;
+    TriRec* tq = nullptr;
+    float* pos = nullptr;
+    float* nrm = nullptr;
+    float* col = nullptr;
+    uint32_t* tris = nullptr;
+    DevCounters* ctr = nullptr;         // two sets, alternating runs
+    uint32_t* totals = nullptr;         // 8 words of the last run's totals (k_finish), for RCCL
+    DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
+    DevCounters* hostCtrDev = nullptr;  // its device address
+    uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
+    uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
+    hipEvent_t ev[kNumKernels + 1] = {};
+    int useGraph = 0;  // replay repeated launch sequences from a hipGraph (measured slower on ROCm 7.2)
+    struct GraphSlot {
+        hipGraphExec_t exec = nullptr;
+        JitKernels* jit = nullptr;
+        Params key{};
+        uint32_t shape[3] = {0, 0, 0};
+    } graphs[2];
+    float lastMs[kNumKernels] = {};
+    PsMeshInfo info{};
+    // high-water marks of finished runs: the next run's buffers are sized from them
+    // (an animation whose mesh grows frame to frame does not pay a synchronous re-run)
+    uint32_t seenV = 0, seenT = 0, seenShardV = 0, seenShardT = 0;
+};
+
+
+namespace psgpu {
+// HIP error -> library return code (prints the failing call).
+int hip_fail(hipError_t e, const char* what);
+// Make the context's device current on the calling thread.
+int set_device(psgpu_ctx* c);
+}  // namespace psgpu
+
+#define PSGPU_CHECK(expr)                                           \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return psgpu::hip_fail(_e, #expr);    \
+    } while (0)

@@ -50,6 +50,17 @@ __global__ void __launch_bounds__(256) k_finish(Params p) {
     finish_body<InterpEval>(p, flds);
 }
 
+// Gathered parts of one grid (psgpu_group_gather): a part's triangles get its vertex
+// base added to their ids and its MPU offsets (V | T << 32) its (vertex, triangle)
+// bases, so the concatenation is the single-device mesh.  One u32 / u64 per lane,
+// 4 per thread, grid-stride.
+__global__ void __launch_bounds__(256) k_rebase(uint32_t* __restrict__ tris, uint64_t nTri, uint32_t vBase,
+                                                uint64_t* __restrict__ offs, uint64_t nOff, uint64_t offBase) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nTri; i += stride) tris[i] += vBase;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nOff; i += stride) offs[i] += offBase;
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (psgpu_launch.h).
 size_t mpu_lds_bytes(uint32_t slots) { return kLdsTables + 4 * (kLdsSlots + (size_t)slots * 64 * 4); }
@@ -78,6 +89,16 @@ hipError_t launch_probe(const Params& p, hipStream_t s, const float* xyz, float*
     const uint32_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(k_probe, dim3(blocks ? blocks : 1), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p, xyz,
                        out, col, n, mode);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebase(uint32_t* tris, uint64_t nTri, uint32_t vBase, uint64_t* offs, uint64_t nOff,
+                         uint64_t offBase, hipStream_t s) {
+    const uint64_t n = nTri > nOff ? nTri : nOff;
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 1023) / 1024;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_rebase, dim3((uint32_t)blocks), dim3(256), 0, s, tris, nTri, vBase, offs, nOff, offBase);
     return hipGetLastError();
 }
 

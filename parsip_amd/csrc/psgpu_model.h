@@ -204,6 +204,8 @@ struct Params {
     DevCounters* ctr;       // this run's counters (two sets alternate between runs)
     DevCounters* ctrNext;   // the next run's, reset by k_finish
     DevCounters* hostCtr;   // host-mapped copy written by k_finish
+    uint32_t* totals;       // 8 words written by k_finish: MPUs, V, T, passed S1, surface MPUs,
+                            // S2 MPUs, first overflow MPU, error (the parts' count exchange)
     uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
     uint32_t debug;         // ablation switches for profiling (0 in production)
 };

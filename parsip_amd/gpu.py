@@ -34,6 +34,12 @@ class PsMeshInfo(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class PsGroupPart(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("mpuBegin", ctypes.c_uint32), ("mpuEnd", ctypes.c_uint32),
+                ("vertexBase", ctypes.c_uint32), ("triangleBase", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("info", PsMeshInfo)]
+
+
 class PsMeshDevice(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "nrm", "col", "tris", "mpuOffsets")]
 
@@ -44,7 +50,13 @@ EXPORTED_SYMBOLS = [
     "psgpu_set_model", "psgpu_polygonize", "psgpu_finish", "psgpu_mesh_device", "psgpu_download_mesh",
     "psgpu_download_stats", "psgpu_export_polympus", "psgpu_polygonize_mpus", "psgpu_last_kernel_times",
     "psgpu_field_values", "psgpu_set_option", "psgpu_jit_active", "psgpu_jit_source", "psgpu_jit_compile",
-    "psgpu_jit_pending", "psgpu_jit_wait",
+    "psgpu_jit_pending", "psgpu_jit_wait", "psgpu_mpu_costs", "psgpu_split_costs",
+    "psgpu_group_create", "psgpu_group_destroy", "psgpu_group_size", "psgpu_group_context",
+    "psgpu_group_set_option", "psgpu_group_set_model", "psgpu_group_jit_wait", "psgpu_group_set_split",
+    "psgpu_group_get_split", "psgpu_group_polygonize", "psgpu_group_finish", "psgpu_group_download_mesh",
+    "psgpu_group_gather", "psgpu_group_export_polympus", "psgpu_group_polygonize_mpus",
+    "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
+    "psgpu_comm_result",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -57,6 +69,9 @@ OPT_CAPACITY = 6
 OPT_GRAPH = 7
 OPT_BOUND = 10
 OPT_JIT_ASYNC = 11
+GROUP_OPT_BALANCE = 100
+BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3
+COMM_ID_BYTES = 128
 
 
 def load(build_if_missing: bool = True):
@@ -95,6 +110,28 @@ def load(build_if_missing: bool = True):
         "psgpu_jit_wait": ([vp], i32),
         "psgpu_jit_source": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "psgpu_jit_compile": ([vp, vp, vp, i32, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
+        "psgpu_mpu_costs": ([vp, vp], i32),
+        "psgpu_split_costs": ([vp, u32, u32, u32, vp], i32),
+        "psgpu_group_create": ([vp, i32, ctypes.POINTER(vp)], i32),
+        "psgpu_group_destroy": ([vp], None),
+        "psgpu_group_size": ([vp], i32),
+        "psgpu_group_context": ([vp, i32], vp),
+        "psgpu_group_set_option": ([vp, i32, ctypes.c_int64], i32),
+        "psgpu_group_set_model": ([vp, vp, vp, vp], i32),
+        "psgpu_group_jit_wait": ([vp], i32),
+        "psgpu_group_set_split": ([vp, vp], i32),
+        "psgpu_group_get_split": ([vp, vp], i32),
+        "psgpu_group_polygonize": ([vp, f32], i32),
+        "psgpu_group_finish": ([vp, ctypes.POINTER(PsMeshInfo), vp], i32),
+        "psgpu_group_download_mesh": ([vp, vp, vp, vp, vp, vp], i32),
+        "psgpu_group_gather": ([vp, i32, ctypes.POINTER(PsMeshDevice)], i32),
+        "psgpu_group_export_polympus": ([vp, vp, u32, ctypes.POINTER(u32)], i32),
+        "psgpu_group_polygonize_mpus": ([vp, f32, vp, vp, vp, vp, u32, ctypes.POINTER(u32)], i32),
+        "psgpu_comm_unique_id": ([vp], i32),
+        "psgpu_comm_create": ([vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
+        "psgpu_comm_destroy": ([vp], None),
+        "psgpu_comm_exchange": ([vp, vp], i32),
+        "psgpu_comm_result": ([vp, ctypes.POINTER(PsMeshInfo), vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -148,6 +185,14 @@ def jit_compile(model: soa.Model, mode: int = 1) -> int:
 
 def device_count() -> int:
     return int(load().psgpu_device_count())
+
+
+def split_costs(costs: np.ndarray, parts: int, begin: int = 0) -> np.ndarray:
+    """Contiguous MPU ranges of near-equal cost (host only): bounds[0..parts]."""
+    c = np.ascontiguousarray(costs, np.uint32)
+    b = np.zeros(parts + 1, np.uint32)
+    _check(load().psgpu_split_costs(c.ctypes.data, len(c), parts, begin, b.ctypes.data), "psgpu_split_costs")
+    return b
 
 
 @dataclass
@@ -267,6 +312,19 @@ class Polygonizer:
         _check(self._L.psgpu_mesh_device(self._ctx, ctypes.byref(d)), "psgpu_mesh_device")
         return d
 
+    def mpu_costs(self) -> np.ndarray:
+        """Per-MPU lane-evaluations of the last run (balances ranges across devices)."""
+        info = self.finish()
+        c = np.zeros(max(info.ctMPUs, 1), np.uint32)
+        _check(self._L.psgpu_mpu_costs(self._ctx, c.ctypes.data), "psgpu_mpu_costs")
+        return c[:info.ctMPUs]
+
+    def plan_split(self, cellsize: float, parts: int) -> np.ndarray:
+        """Cost split of the whole lattice into `parts` ranges from one full run on this
+        context (deterministic: every rank computes the same split)."""
+        self.run(cellsize)
+        return split_costs(self.mpu_costs(), parts)
+
     def kernel_times(self) -> dict:
         ms = (ctypes.c_float * 8)()
         names = (ctypes.c_char_p * 8)()
@@ -306,3 +364,125 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
     rc = ctx._L.psgpu_polygonize_mpus(ctx._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
                                       ctypes.byref(ct), None if stats is None else stats.ctypes.data)
     return rc, ct.value, poly_mpus
+
+
+def _mesh_from_arrays(V, T, N, fill):
+    pos = np.zeros((V, 3), np.float32)
+    nrm = np.zeros((V, 3), np.float32)
+    col = np.zeros((V, 3), np.float32)
+    tris = np.zeros((T, 3), np.uint32)
+    off = np.zeros(N + 1, np.uint64)
+    fill(pos, nrm, col, tris, off)
+    return Mesh(pos, nrm, col, tris, (off & 0xFFFFFFFF).astype(np.int64), (off >> 32).astype(np.int64))
+
+
+class Group:
+    """One MPU lattice over several device contexts (psgpu_group_*): contiguous ranges of
+    near-equal cost, all devices launched at once; the parts concatenate to the
+    single-device mesh."""
+
+    def __init__(self, devices):
+        L = load()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        self._g = ctypes.c_void_p()
+        _check(L.psgpu_group_create(devs, len(devices), ctypes.byref(self._g)), "psgpu_group_create")
+        self._L = L
+        self.n = len(devices)
+
+    def close(self):
+        if getattr(self, "_g", None) and self._g.value:
+            self._L.psgpu_group_destroy(self._g)
+            self._g = ctypes.c_void_p()
+
+    __del__ = close
+
+    def set_option(self, option: int, value: int) -> None:
+        _check(self._L.psgpu_group_set_option(self._g, option, value), "psgpu_group_set_option")
+
+    def set_model(self, model: soa.Model, wait_jit: bool = True) -> None:
+        _check(self._L.psgpu_group_set_model(self._g, *model.ptrs()), "psgpu_group_set_model")
+        if wait_jit:
+            self._L.psgpu_group_jit_wait(self._g)
+
+    def set_split(self, bounds) -> None:
+        b = np.ascontiguousarray(bounds, np.uint32)
+        assert len(b) == self.n + 1
+        _check(self._L.psgpu_group_set_split(self._g, b.ctypes.data), "psgpu_group_set_split")
+
+    def split(self) -> np.ndarray:
+        b = np.zeros(self.n + 1, np.uint32)
+        _check(self._L.psgpu_group_get_split(self._g, b.ctypes.data), "psgpu_group_get_split")
+        return b
+
+    def polygonize(self, cellsize: float) -> None:
+        _check(self._L.psgpu_group_polygonize(self._g, cellsize), "psgpu_group_polygonize")
+
+    def finish(self):
+        info = PsMeshInfo()
+        parts = (PsGroupPart * self.n)()
+        _check(self._L.psgpu_group_finish(self._g, ctypes.byref(info), parts), "psgpu_group_finish")
+        return info, list(parts)
+
+    def run(self, cellsize: float):
+        self.polygonize(cellsize)
+        return self.finish()
+
+    def download(self) -> Mesh:
+        info, _ = self.finish()
+
+        def fill(pos, nrm, col, tris, off):
+            _check(self._L.psgpu_group_download_mesh(self._g, pos.ctypes.data, nrm.ctypes.data, col.ctypes.data,
+                                                     tris.ctypes.data, off.ctypes.data), "psgpu_group_download_mesh")
+        return _mesh_from_arrays(info.ctVertices, info.ctTriangles, info.ctMPUs, fill)
+
+    def gather(self, dst_part: int = 0) -> PsMeshDevice:
+        d = PsMeshDevice()
+        _check(self._L.psgpu_group_gather(self._g, dst_part, ctypes.byref(d)), "psgpu_group_gather")
+        return d
+
+    def export_polympus(self, capacity: int | None = None) -> np.ndarray:
+        info, _ = self.finish()
+        cap = info.ctMPUs if capacity is None else capacity
+        out = np.zeros(max(cap, 1), soa.MPU_DTYPE)
+        ct = ctypes.c_uint32()
+        _check(self._L.psgpu_group_export_polympus(self._g, out.ctypes.data, cap, ctypes.byref(ct)),
+               "psgpu_group_export_polympus")
+        return out[:ct.value]
+
+    def context_ptr(self, part: int):
+        return self._L.psgpu_group_context(self._g, part)
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    _check(load().psgpu_comm_unique_id(buf), "psgpu_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """RCCL count exchange of one rank's polygonization (one process per GPU)."""
+
+    def __init__(self, poly: Polygonizer, uid: bytes, nranks: int, rank: int):
+        assert len(uid) == COMM_ID_BYTES
+        self._L = load()
+        self._poly = poly
+        self.nranks = nranks
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        self._c = ctypes.c_void_p()
+        _check(self._L.psgpu_comm_create(poly._ctx, buf, nranks, rank, ctypes.byref(self._c)), "psgpu_comm_create")
+
+    def close(self):
+        if getattr(self, "_c", None) and self._c.value:
+            self._L.psgpu_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    __del__ = close
+
+    def exchange(self) -> None:
+        _check(self._L.psgpu_comm_exchange(self._c, self._poly._ctx), "psgpu_comm_exchange")
+
+    def result(self):
+        info = PsMeshInfo()
+        parts = (PsGroupPart * self.nranks)()
+        _check(self._L.psgpu_comm_result(self._c, ctypes.byref(info), parts), "psgpu_comm_result")
+        return info, list(parts)

@@ -1,0 +1,182 @@
+"""One grid over several parts, on the HIP path.
+
+The reference's Polygonize fans the MPU list over every core in one call
+(PS_Polygonizer.cpp:379-382); psgpu_group_* fans it over device contexts and
+psgpu_comm_* exchanges the parts' counts over RCCL when there is one process per GPU.
+On the one-GPU test box the parts share device 0 (a group may put several parts on one
+device); the reassembled mesh must equal the committed single-device oracle digests.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from parity_util import assert_bits_equal, assert_mesh_matches, mesh_digests
+from parsip_amd import gpu, soa, synth
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _stats4(polys_stats):
+    st = np.concatenate(polys_stats)
+    return np.stack([st["passedPrecheck"], st["ctFieldEvals"], st["ctVertices"], st["ctTriangles"]], axis=1)
+
+
+def _group_stats(group):
+    return [group_ctx_stats(group, p) for p in range(group.n)]
+
+
+def group_ctx_stats(group, part):
+    """PsMpuStats of one part through the C-ABI (psgpu_download_stats on its context)."""
+    L = gpu.load()
+    info, parts = group.finish()
+    n = parts[part].info.ctMPUs
+    st = np.zeros(max(n, 1), soa.MPU_STATS_DTYPE)
+    rc = L.psgpu_download_stats(group.context_ptr(part), st.ctypes.data)
+    assert rc == soa.RET_SUCCESS
+    return st[:n]
+
+
+@pytest.fixture(scope="module")
+def group8():
+    assert gpu.device_count() > 0, "no HIP device visible"
+    g = gpu.Group([0] * 8)
+    yield g
+    g.close()
+
+
+def test_group_c3_eight_balanced_parts_equal_golden(group8):
+    """C4 rehearsal: C3 as 8 cost-balanced ranges (planning run + split), reassembled."""
+    model, cs, _ = synth.make_config("C3")
+    group8.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+    group8.set_model(model)
+    info, parts = group8.run(cs)
+    bounds = group8.split()
+    assert bounds[0] == 0 and bounds[-1] == info.ctMPUs == 50653
+    assert all(parts[p].mpuBegin == bounds[p] and parts[p].mpuEnd == bounds[p + 1] for p in range(8))
+    # balanced by cost: lane-evaluations per part within 15 % of the mean
+    evals = np.array([p.info.ctLaneEvals for p in parts], np.float64)
+    assert evals.max() / evals.mean() < 1.15, evals
+    dig = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["C3"]
+    mesh = group8.download()
+    got = mesh_digests(_stats4(_group_stats(group8)), mesh.pos, mesh.nrm, mesh.col, mesh.local_tris())
+    assert got == dig
+    # the device gather (peer copies + rebase kernel) equals the host reassembly
+    d = group8.gather(0)
+    import ctypes
+
+    L = gpu.load()
+    V, T = info.ctVertices, info.ctTriangles
+    pos = np.zeros((V, 3), np.float32)
+    tris = np.zeros((T, 3), np.uint32)
+    offs = np.zeros(info.ctMPUs + 1, np.uint64)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(pos.ctypes.data, d.pos, pos.nbytes, 2) == 0
+    assert hip.hipMemcpy(tris.ctypes.data, d.tris, tris.nbytes, 2) == 0
+    assert hip.hipMemcpy(offs.ctypes.data, d.mpuOffsets, offs.nbytes, 2) == 0
+    assert_bits_equal(pos, mesh.pos, "gathered positions")
+    np.testing.assert_array_equal(tris, mesh.tris)
+    np.testing.assert_array_equal((offs & 0xFFFFFFFF).astype(np.int64), mesh.vertex_offsets)
+    np.testing.assert_array_equal((offs >> 32).astype(np.int64), mesh.triangle_offsets)
+    assert L is not None
+
+
+@pytest.mark.parametrize("policy", [gpu.BALANCE_EVEN, gpu.BALANCE_EVERY_RUN])
+def test_group_c2_policies_match_oracle(group8, oracle, policy):
+    model, cs, _ = synth.make_config("C2")
+    group8.set_option(gpu.GROUP_OPT_BALANCE, policy)
+    group8.set_model(model)
+    for _ in range(2):  # EVERY_RUN re-splits after the first finish
+        group8.run(cs)
+    mesh = group8.download()
+    om = oracle.polygonize(model, cs, threads=8)
+    st = np.concatenate(_group_stats(group8))
+    assert_mesh_matches(mesh, st, om)
+
+
+def test_group_fixed_split_with_empty_parts(group8, oracle):
+    model, cs, _ = synth.make_config("C2")
+    n = gpu.count_mpus(cs, *model.bbox)
+    group8.set_model(model)
+    group8.set_split([0, 0, 17, 17, n // 2, n // 2 + 1, n - 3, n, n])
+    info, parts = group8.run(cs)
+    assert [p.mpuEnd - p.mpuBegin for p in parts] == [0, 17, 0, n // 2 - 17, 1, n - 3 - n // 2 - 1, 3, 0]
+    mesh = group8.download()
+    om = oracle.polygonize(model, cs, threads=8)
+    assert_mesh_matches(mesh, np.concatenate(_group_stats(group8)), om)
+
+
+def test_group_export_polympus_equals_single_context(group8, gpu_poly):
+    model, cs, _ = synth.make_config("C2")
+    group8.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+    group8.set_model(model)
+    group8.run(cs)
+    a = group8.export_polympus()
+    gpu_poly.set_model(model)
+    gpu_poly.run(cs)
+    b = gpu_poly.export_polympus()
+    assert a.tobytes() == b.tobytes()
+    # the reference capacity of PolyMPUs (24,000) is too small for 50,653 MPUs: -4, no export
+    model3, cs3, _ = synth.make_config("C3")
+    group8.set_model(model3)
+    group8.run(cs3)
+    with pytest.raises(gpu.PsgpuError) as e:
+        group8.export_polympus(capacity=soa.MAX_MPU_COUNT)
+    assert e.value.code == -4
+
+
+def test_rccl_exchange_single_rank(gpu_poly):
+    """The RCCL path of the multi-process form at world size 1 (one GPU on this box)."""
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+    comm = gpu.Comm(gpu_poly, gpu.comm_unique_id(), 1, 0)
+    try:
+        for _ in range(3):
+            gpu_poly.polygonize(cs)
+            comm.exchange()
+        total, parts = comm.result()
+        info = gpu_poly.finish()
+        assert (total.ctMPUs, total.ctVertices, total.ctTriangles, total.ctPassedPrecheck) == \
+            (info.ctMPUs, info.ctVertices, info.ctTriangles, info.ctPassedPrecheck)
+        assert parts[0].vertexBase == 0 and parts[0].mpuEnd == info.ctMPUs
+    finally:
+        comm.close()
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ, **(env_extra or {}))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_contract_one_gpu():
+    out = _bench(["--steps", "5", "--warmup", "1", "--no-cpu"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in out, k
+    assert out["n_gpus"] == 1 and out["steps"] == 5 and out["warmup"] == 1
+    assert out["mesh"]["vertices"] == 339820 and out["mesh"]["triangles"] == 520224
+    assert 0 < out["roofline"]["frac"] <= 1 and out["roofline"]["bound"] == "valu"
+    assert out["value"] > 0
+
+
+def test_bench_two_ranks_strong_split_one_device():
+    """`bench.py --gpus 2` spawns its two ranks itself; pinned to device 0 they split the one
+    256^3 grid and their parts must add up to the full grid (checked inside the bench)."""
+    out = _bench(["--gpus", "2", "--steps", "5", "--warmup", "1", "--no-cpu"], {"PSGPU_BENCH_DEVICE": "0"})
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert out["check"]["parts_sum_to_full_grid"] is True
+    per = out["mesh"]["per_rank"]
+    assert sum(p[1] for p in per) == 339820 and sum(p[2] for p in per) == 520224
+    assert sum(p[0] for p in per) == 50653
