@@ -210,6 +210,14 @@ int  psgpu_polygonize_mpus(psgpu_ctx* ctx, float cellsize, const PsSoaBlobPrims*
                            const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops,
                            PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs,
                            PsMpuStats* statsOrNull);
+/* Per-wave timeline of the last polygonize (PSGPU_OPT_STAMPS > 0; the reference's
+ * MPUSTATS / PrintThreadResults, PS_Polygonizer.h:201-207, .cpp:414-461, with waves for
+ * threads): 4 kernels (precheck, mpu, vertex, finish) x cap records of 3 uint64:
+ * start, end (100 MHz s_memrealtime ticks), item | hw id << 32 where item is the MPU a
+ * k_mpu wave polygonized (0xffffffff: none) or the wave's index, hw id = HW_ID[15:0] |
+ * XCC_ID << 16.  Unlaunched waves read zero; then cap x 8 words of k_mpu phase stamps
+ * (PSGPU_OPT_DEBUG bit 4096; profiling only).  Pass out = NULL to query *cap. */
+int  psgpu_download_stamps(psgpu_ctx* ctx, uint64_t* out, uint32_t* cap);
 /* Device-side timing of the last polygonize, per kernel (ms); returns count filled. */
 int  psgpu_last_kernel_times(psgpu_ctx* ctx, float* ms, int maxKernels, const char** names);
 /* FieldComputer::fieldValue / fieldValueAndColor on n host points (xyz interleaved):
@@ -232,6 +240,8 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        output unchanged; JIT kernels only) */
 #define PSGPU_OPT_JIT           3   /* 0 interpreter, 1 specialised per structure (default),
                                        2 specialised with parameters baked in */
+#define PSGPU_OPT_STAMPS       12   /* > 0: record a per-wave timeline for up to this many waves
+                                       per kernel (psgpu_download_stamps); 0: off (default) */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the
                                        specialised kernels on a host thread while the interpreter
                                        serves polygonizations (bit-identical output); 0: block */

@@ -289,69 +289,75 @@ struct CullMask {
     uint64_t lo, hi;
 };
 
-// Lower bound of the primitive's distance from c, and (axis clearance) the distance
-// of c from the segment's infinite line.
-__device__ __forceinline__ float cull_dist(const CullSeg& S, uint32_t flags, float cx, float cy, float cz,
-                                           float* lineDist) {
-    const float dx = cx - S.a[0], dy = cy - S.a[1], dz = cz - S.a[2];
-    const float t = (dx * S.u[0] + dy * S.u[1] + dz * S.u[2]) * S.invUU;
-    const float lx = dx - t * S.u[0], ly = dy - t * S.u[1], lz = dz - t * S.u[2];
-    *lineDist = __builtin_amdgcn_sqrtf(lx * lx + ly * ly + lz * lz);
-    const float tc = (flags & 2u) ? t : fminf(fmaxf(t, 0.0f), 1.0f);
-    const float ex = dx - tc * S.u[0], ey = dy - tc * S.u[1], ez = dz - tc * S.u[2];
-    return __builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez) - S.radius;
-}
+// This lane's culling segments (prims `lane` and 64 + `lane`), loaded once and early: the
+// loads do not depend on the box, so they overlap the rest of a kernel's prologue.
+struct CullLanes {
+    CullSeg s[2];
+    bool two;  // ctPrims > 64
+};
 
 __device__ __forceinline__ CullSeg load_cullseg(ModelPtr M, int i) {
-    const CullSeg __attribute__((address_space(4)))& src = M->cull[i];
+    typedef const __attribute__((address_space(4))) float* CF;
+    const CF f = (CF)(&M->cull[i]);  // 12 consecutive floats: the compiler emits 16-B loads
     CullSeg S;
-    S.a[0] = src.a[0]; S.a[1] = src.a[1]; S.a[2] = src.a[2];
-    S.u[0] = src.u[0]; S.u[1] = src.u[1]; S.u[2] = src.u[2];
-    S.invUU = src.invUU;
-    S.radius = src.radius;
+    S.a[0] = f[0]; S.a[1] = f[1]; S.a[2] = f[2];
+    S.u[0] = f[3]; S.u[1] = f[4]; S.u[2] = f[5];
+    S.invUU = f[6]; S.radius = f[7];
+    S.tmin = f[8]; S.tmax = f[9]; S.axisClear = f[10]; S.pad = f[11];
     return S;
 }
 
-__device__ __forceinline__ CullMask cull_mask_box(ModelPtr M, float x0, float y0, float z0, float x1, float y1,
-                                                  float z1) {
+__device__ __forceinline__ CullLanes load_cull_lanes(ModelPtr M) {
+    CullLanes L;
+    L.two = M->ctPrims > 64u;
+    L.s[0] = load_cullseg(M, lane_id());
+    if (L.two) L.s[1] = load_cullseg(M, 64 + lane_id());
+    return L;
+}
+
+// Is the segment's primitive exactly +0 over the box (centre c, half-diagonal h)?
+__device__ __forceinline__ bool cull_one(const CullSeg& S, float cx, float cy, float cz, float h) {
+    const float dx = cx - S.a[0], dy = cy - S.a[1], dz = cz - S.a[2];
+    const float t = (dx * S.u[0] + dy * S.u[1] + dz * S.u[2]) * S.invUU;
+    const float lx = dx - t * S.u[0], ly = dy - t * S.u[1], lz = dz - t * S.u[2];
+    const float lineDist = __builtin_amdgcn_sqrtf(lx * lx + ly * ly + lz * lz);
+    const float tc = fminf(fmaxf(t, S.tmin), S.tmax);
+    const float ex = dx - tc * S.u[0], ey = dy - tc * S.u[1], ez = dz - tc * S.u[2];
+    const float d = (__builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez) - S.radius) - h;
+    return d > 0.0f && d * d >= 1.02f && (lineDist - h > S.axisClear);
+}
+
+__device__ __forceinline__ CullMask cull_mask_from(const CullLanes& L, float x0, float y0, float z0, float x1,
+                                                   float y1, float z1) {
     CullMask cm{0ull, 0ull};
     if (!(x1 - x0 < 1e30f && y1 - y0 < 1e30f && z1 - z0 < 1e30f)) return cm;
     const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), cz = 0.5f * (z0 + z1);
     const float hx = 0.5f * (x1 - x0), hy = 0.5f * (y1 - y0), hz = 0.5f * (z1 - z0);
     const float h = __builtin_amdgcn_sqrtf(hx * hx + hy * hy + hz * hz) * 1.0001f + 1e-6f;
-    const int n = (int)M->ctPrims;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        const int i = half * 64 + lane_id();
-        bool cull = false;
-        if (i < n) {
-            CPrim& P = M->prims[i];
-            const uint32_t fl = P.cullable;
-            if (fl & 1u) {
-                float ld;
-                const CullSeg S = load_cullseg(M, i);
-                const float d = cull_dist(S, fl, cx, cy, cz, &ld) - h;
-                cull = d > 0.0f && d * d >= 1.02f;
-                if (fl & 4u) cull = cull && (ld - h > 0.05f);
-            } else if (P.type == PSGPU_T_TRIANGLE) {
-                cull = true;
-            }
-        }
-        const uint64_t b = ballot(cull);
-        if (half == 0) cm.lo = b; else cm.hi = b;
-    }
+    cm.lo = ballot(cull_one(L.s[0], cx, cy, cz, h));
+    if (L.two) cm.hi = ballot(cull_one(L.s[1], cx, cy, cz, h));
     return cm;
+}
+
+__device__ __forceinline__ CullMask cull_mask_box(ModelPtr M, float x0, float y0, float z0, float x1, float y1,
+                                                  float z1) {
+    return cull_mask_from(load_cull_lanes(M), x0, y0, z0, x1, y1, z1);
 }
 
 // Cull mask for the AABB of this wave's points (all 64 lanes must participate),
 // optionally grown by `ext` on the high side of every axis.
-__device__ __forceinline__ CullMask cull_mask_points(ModelPtr M, float px, float py, float pz, bool enable,
+__device__ __forceinline__ CullMask cull_mask_points(const CullLanes& L, float px, float py, float pz, bool enable,
                                                      float ext = 0.0f) {
     if (!enable) return CullMask{0ull, 0ull};
     // a NaN coordinate (fminf/fmaxf would hide it) disables culling for the wave
     if (ballot(!(px == px) || !(py == py) || !(pz == pz)) != 0ull) return CullMask{0ull, 0ull};
-    return cull_mask_box(M, wave_min(px), wave_min(py), wave_min(pz), wave_max(px) + ext, wave_max(py) + ext,
-                         wave_max(pz) + ext);
+    return cull_mask_from(L, wave_min(px), wave_min(py), wave_min(pz), wave_max(px) + ext, wave_max(py) + ext,
+                          wave_max(pz) + ext);
+}
+__device__ __forceinline__ CullMask cull_mask_points(ModelPtr M, float px, float py, float pz, bool enable,
+                                                     float ext = 0.0f) {
+    if (!enable) return CullMask{0ull, 0ull};
+    return cull_mask_points(load_cull_lanes(M), px, py, pz, true, ext);
 }
 
 __device__ __forceinline__ bool culled(const CullMask& cm, uint32_t i) {
@@ -586,6 +592,43 @@ struct InterpEval {
 };
 
 // ---------------------------------------------------------------------------
+// Per-wave timeline (the reference's MPUSTATS / PrintThreadResults, PS_Polygonizer.h:201-207,
+// .cpp:414-461, with waves for threads): when p.stamps is set every wave of kernel K
+// records {start, end, item | hw id << 32} in the 100 MHz s_memrealtime clock, item = the
+// MPU a k_mpu wave polygonized (0xffffffff: none) or the wave's global index.
+__device__ __forceinline__ uint64_t stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_end(const Params& p, int K, uint64_t t0, uint32_t item) {
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= p.stampCap) return;
+    const uint64_t t1 = stamp_now();
+    // HW_ID (CU, SIMD, SE; 32 bits) and XCC_ID (hwreg 20) as one word: hwid[15:0] | xcc << 16
+    const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 15u;
+    if (lane_id() == 0) {
+        uint64_t* r = p.stamps + 3 * ((size_t)K * p.stampCap + w);
+        r[0] = t0;
+        r[1] = t1;
+        r[2] = (uint64_t)item | ((uint64_t)((hw & 0xffffu) | (xcc << 16)) << 32);
+    }
+}
+// Phase stamps inside one wave (debug bit 4096, k_mpu): 8 words per wave after the
+// kernels' records; phase 0 = entry.
+__device__ __forceinline__ void phase_stamp(const Params& p, int ph) {
+    if (!(p.debug & 4096u) || !p.stamps) return;
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= p.stampCap) return;
+    const uint64_t t = stamp_now();
+    if (lane_id() == 0) p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)w + ph] = t;
+}
+#define PSGPU_STAMPED(K, ITEM, CALL)                                             \
+    {                                                                             \
+        const uint64_t t0_ = p.stamps ? psgpu::stamp_now() : 0ull;                \
+        uint32_t item_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);     \
+        CALL;                                                                     \
+        if (p.stamps) psgpu::stamp_end(p, K, t0_, ITEM);                          \
+    }
+
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ void mpu_origin(const Params& p, uint32_t m, float o[3]) {
     const uint32_t k = m % p.dims[2];
     const uint32_t j = (m / p.dims[2]) % p.dims[1];
@@ -609,6 +652,8 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
+    CullLanes cl;  // loaded first: independent of everything below
+    if (p.cull) cl = load_cull_lanes(as_const(p.model));
     const uint32_t W = blockIdx.x * 4u + (uint32_t)wave;
     const uint32_t bzN = p.brickDims[2], byN = p.brickDims[1];
     const uint32_t nBricks = p.brickDims[0] * byN * bzN;
@@ -630,10 +675,10 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     float f = -1.0f;
     CullMask cm{0ull, 0ull};
     if (!(p.debug & 8u)) {  // ablation bit 3: S1 without the walk (nothing passes)
-        cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+        cm = cull_mask_points(cl, px, py, pz, p.cull != 0);
         f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
     } else if (p.debug & 16u) {  // bit 4: the culling mask only
-        cm = cull_mask_points(as_const(p.model), px, py, pz, p.cull != 0);
+        cm = cull_mask_points(cl, px, py, pz, p.cull != 0);
         f = (float)(cm.lo & 1ull) - 1.0f;
     }
     const uint64_t bal = ballot(valid && f > 0.0f);
@@ -644,6 +689,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     // the 4x4x4 corners [4X, 4X+3] x [4Y, 4Y+3] x [4Z, 4Z+3] of its S2 cache (its z range
     // is exactly one S2 quad); the wave's culling box covers every MPU of the brick.
     uint32_t proven8 = 0;
+    if ((p.debug & 1024u) && flags8 != 0u) __builtin_amdgcn_s_setprio(2);  // experiment: heavy waves first
     if (p.bound && flags8 != 0u) {
         BoundBox B;
 #pragma unroll
@@ -689,21 +735,22 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
 }
 
 #ifndef PSGPU_S2_N
-#define PSGPU_S2_N 8  // x-slices per walk in S2 (1, 2, 4 or 8): one walk per (y,z) needle
-                      // shares each primitive's uniform work and (y,z) terms over 8 points
+#define PSGPU_S2_N (8 / PSGPU_MPU_WAVES)  // x-slices per walk: one walk per (y,z) needle shares each
+                                          // primitive's uniform work and (y,z) terms over its points
 #endif
+// LDS per k_mpu block: per MPU of the block (4 / W of them): edgeVid[1536] u16 (passes 2-3) | cfg[344] u8 | vbase[344] u16 |
+// tbase[344] u16 | the 8 inside-bit words of the S2 cache | qv, qt; then per wave the
+// interpreter's value slots.  The S2 field values never leave registers: pass 1 needs
+// only their inside bits (8 ballots, shared by the MPU's waves through LDS).
 constexpr int kLdsEdge = 0;
 constexpr int kLdsCfg = kLdsEdge + 1536 * 2;
 constexpr int kLdsVbase = kLdsCfg + 344;
 constexpr int kLdsTbase = kLdsVbase + 344 * 2;
-constexpr int kLdsSlots = ((kLdsTbase + 344 * 2) + 15) & ~15;
-
-// Per-MPU body: one wavefront per MPU that passed S1, 4 wavefronts per block.
-// LDS per block: the packed cube tables (shared), then per wave: edgeVid[1536] u16
-// (passes 2-3) | cfg[344] u8 | vbase[344] u16 | tbase[344] u16 | value slots
-// (interpreter).  The S2 field cache never leaves registers: pass 1 needs only its
-// inside bits (8 ballots).
+constexpr int kLdsIns = ((kLdsTbase + 344 * 2) + 7) & ~7;
+constexpr int kLdsQ = kLdsIns + 8 * 8;
+constexpr int kLdsMpu = ((kLdsQ + 8) + 15) & ~15;
 constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
+constexpr int kLdsWaveSlots = kMpusPerBlock * kLdsMpu;  // interpreter slots follow
 
 // Last cell c in [0, 343) with first[c] <= r (first[] = exclusive prefix of per-cell
 // counts, non-decreasing, first[0] = 0, so that cell holds item r): binary lifting,
@@ -718,179 +765,237 @@ __device__ __forceinline__ int find_cell(const uint16_t* first, uint32_t r) {
     return lo;
 }
 
+// Barrier of the MPU's waves (the whole block when W > 1; LDS ordering within the wave
+// when one wave does it all).
+__device__ __forceinline__ void mpu_sync() {
+    if (kMpuWaves > 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Per-MPU body: W = kMpuWaves wavefronts per MPU that passed S1 (and was not proven
+// empty), 4 wavefronts per block.  Every wave of a block reaches every barrier: waves
+// without an MPU (past the last survivor) or whose MPU has no surface just skip the work.
 template <class EV>
-__device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
+__device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, uint32_t* item) {
+    *item = 0xffffffffu;
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
-    // block b, wave v: entry (b % B) * 4 + v of survivor shard b / B, B = pShardCap / 4
-    const uint32_t bps = p.pShardCap / 4u;
-    const uint32_t pshard = blockIdx.x / bps;
-    const uint32_t pidx = (blockIdx.x % bps) * 4u + (uint32_t)wave;
-    const uint32_t pcount = p.ctr->shard[pshard].p;
-    if ((blockIdx.x % bps) * 4u >= pcount) return;  // whole block past the shard's end
-    // stage the tables in LDS (every wave of the block takes part before any exits)
-    CubeTablesDev* tab = reinterpret_cast<CubeTablesDev*>(smem);
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tables);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-        for (int i = threadIdx.x; i < (int)(sizeof(CubeTablesDev) / 4); i += blockDim.x) dst[i] = src[i];
+    const int slot = wave / kMpuWaves;  // the block's MPU this wave works on
+    const int part = wave % kMpuWaves;  // its share: x-slices [part * NX, part * NX + NX)
+    constexpr int NX = 8 / kMpuWaves;
+    // MPU d = block * (4 / W) + slot is the d-th queued survivor in shard order (dense over
+    // the 64 shard queues: lane s holds shard s's count); the grid is sized by the host
+    // from the last finished run, and a run with more survivors than that is re-run by finish()
+    phase_stamp(p, 0);
+    const uint32_t d = blockIdx.x * (uint32_t)kMpusPerBlock + (uint32_t)slot;
+    ModelPtr M = as_const(p.model);
+    const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
+    // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
+    // the block; every lane meanwhile loads its culling segments
+    __shared__ uint32_t sIncl[kShards];
+    if (wave == 0) {
+        const uint32_t cnt = p.ctr->shard[lane].p;  // kShards == 64: one shard per lane
+        sIncl[lane] = wave_incl_scan(cnt);
     }
+    CullLanes cl;
+    if (p.cull) cl = load_cull_lanes(M);
     __syncthreads();
-    if (pidx >= pcount) return;
-    unsigned char* base = smem + kLdsTables + wave * (kLdsSlots + p.slotsPerLane * 64 * 4);
+    // MPU d = block * (4 / W) + slot is the d-th queued survivor in shard order (dense over
+    // the 64 shard queues); the grid is sized by the host from the last finished run, and
+    // a run with more survivors than that is re-run by finish()
+    const uint32_t incl = sIncl[lane];
+    const uint32_t pcount = sIncl[kShards - 1];
+    if (blockIdx.x * (uint32_t)kMpusPerBlock >= pcount) return;  // whole block past the last survivor
+    const bool live = d < pcount;
+    uint32_t m = 0, w = 0;
+    float o[3] = {0.0f, 0.0f, 0.0f};
+    if (live) {
+        const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
+        const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
+        m = __builtin_amdgcn_readfirstlane(p.pq[pshard * p.pShardCap + pidx]);
+        *item = m;
+        w = m - p.mpuBegin;  // slot of the MPU in the range: counts / offsets index
+        mpu_origin(p, m, o);
+    }
+    phase_stamp(p, 1);
+    if (kMpuWaves == 1 && !live) return;
+    unsigned char* base = smem + slot * kLdsMpu;
     uint16_t* edgeVid = reinterpret_cast<uint16_t*>(base + kLdsEdge);
     uint8_t* cellCfg = base + kLdsCfg;
     uint16_t* cellV = reinterpret_cast<uint16_t*>(base + kLdsVbase);
     uint16_t* cellT = reinterpret_cast<uint16_t*>(base + kLdsTbase);
-    ModelPtr M = as_const(p.model);
-    EV ev(M, reinterpret_cast<float*>(base + kLdsSlots) + lane);
-
-    const uint32_t m = __builtin_amdgcn_readfirstlane(p.pq[pshard * p.pShardCap + pidx]);
-    const uint32_t w = m - p.mpuBegin;  // slot of the MPU in the range: counts / offsets index
-    float o[3];
-    mpu_origin(p, m, o);
+    uint64_t* sIns = reinterpret_cast<uint64_t*>(base + kLdsIns);
+    uint32_t* sQ = reinterpret_cast<uint32_t*>(base + kLdsQ);
+    EV ev(M, reinterpret_cast<float*>(smem + kLdsWaveSlots + wave * p.slotsPerLane * 64 * 4) + lane);
     const float cs = p.cs;
 
-    // S2 (:550-610): corner (x, y, z) of the 8x8x8 cache, lane = y*8 + z, 8 x per lane;
-    // quads = 4 consecutive z
-    const int y = lane >> 3, z = lane & 7;
-    const float py = o[1] + (float)y * cs;
-    const float pz = o[2] + (float)z * cs;
-    CullMask cm{0ull, 0ull};
-    if (p.cull) {
-        const float e = 7.0f * cs;
-        cm = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
-    }
-    float pxs[8], pys[8], pzs[8], fs8[8];
+    CullMask cm{0ull, 0ull}, cg{0ull, 0ull};
+    if (live) {
+        // S2 (:550-610): corner (x, y, z) of the 8x8x8 cache, lane = y*8 + z, this wave's
+        // NX x-slices per lane; quads = 4 consecutive z
+        const int y = lane >> 3, z = lane & 7;
+        const float py = o[1] + (float)y * cs;
+        const float pz = o[2] + (float)z * cs;
+        if (p.cull) {
+            const float e = 7.0f * cs;
+            cm = cull_mask_from(cl, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
+            // the MPU box grown by the normal delta, for k_vertex and k_finish (edge samples,
+            // roots, normal samples), stored by the first wave if the MPU has vertices
+            const float eg = 7.0f * cs + 0.001f;
+            if (part == 0) cg = cull_mask_from(cl, o[0], o[1], o[2], o[0] + eg, o[1] + eg, o[2] + eg);
+        }
+        phase_stamp(p, 2);
+        float pxs[NX], pys[NX], pzs[NX], fs[NX];
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-        pxs[x] = o[0] + (float)x * cs;
-        pys[x] = py;
-        pzs[x] = pz;
-    }
+        for (int x = 0; x < NX; ++x) {
+            pxs[x] = o[0] + (float)(part * NX + x) * cs;
+            pys[x] = py;
+            pzs[x] = pz;
+        }
 #if PSGPU_S2_N == 1
-    // one walk per x-slice in a runtime loop: the walk's code stays resident in the
-    // instruction cache (unrolled copies of a 32-primitive walk do not fit)
+        // one walk per x-slice in a runtime loop: the walk's code stays resident in the
+        // instruction cache (unrolled copies of a 32-primitive walk do not fit)
 #pragma unroll 1
-    for (int h = 0; h < 8; ++h) fs8[h] = ev.template eval<4, false>(pxs[h], py, pz, cm, nullptr);
+        for (int h = 0; h < NX; ++h) fs[h] = ev.template eval<4, false>(pxs[h], py, pz, cm, nullptr);
 #else
 #pragma unroll
-    for (int h = 0; h < 8; h += PSGPU_S2_N)
-        ev.template evaln<4, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs8 + h, nullptr);
+        for (int h = 0; h < NX; h += PSGPU_S2_N)
+            ev.template evaln<4, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs + h, nullptr);
 #endif
-    // inside bits of the 8x8x8 corners: ins[x] bit y*8 + z (lane order)
+        // inside bits of the 8x8x8 corners: ins[x] bit y*8 + z (lane order)
+#pragma unroll
+        for (int x = 0; x < NX; ++x) {
+            const uint64_t b = ballot(fs[x] >= 0.5f);
+            if (lane == 0) sIns[part * NX + x] = b;
+        }
+    }
+    phase_stamp(p, 3);
+    mpu_sync();
+    phase_stamp(p, 4);
     uint64_t ins[8];
     uint32_t inside = 0;
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
-        ins[x] = ballot(fs8[x] >= 0.5f);
+        ins[x] = live ? sIns[x] : 0ull;
         inside += __popcll(ins[x]);
     }
-    if (inside == 0 || inside == 512 || (p.debug & 1u)) {  // no vertices, no triangles
-        if (lane == 0) p.counts[w] = 0ull;
-        return;
-    }
+    const bool work = live && inside != 0 && inside != 512 && !(p.debug & 1u);
+    if (live && !work && part == 0 && lane == 0) p.counts[w] = 0ull;  // no vertices, no triangles
+    if (kMpuWaves == 1 && !work) return;
 
     // S3 pass 1 (:647-691): config per cell (bit c = x*4 + y*2 + z, inside = f >= 0.5),
     // owned sign-changing edges (new vertices) and triangles; wave prefix sums give
     // the reference's discovery order over cells (i,j,k): one x-slab i per step, lane
-    // j*8 + k, so the cell's corners are bits lane + {0, 1, 8, 9} of ins[i] and ins[i+1]
+    // j*8 + k, so the cell's corners are bits lane + {0, 1, 8, 9} of ins[i] and ins[i+1].
+    // Every wave of the MPU computes V and T; the first writes the tables and counters.
     const uint64_t edgeBits = tab->edge;
-    uint32_t carryV = 0, carryT = 0;
-    const int j = lane >> 3, k = lane & 7;
-    const bool cellLane = j < 7 && k < 7;
+    uint32_t V = 0, T = 0;
+    if (work) {
+        uint32_t carry = 0;  // V | T << 16 (both <= 343 * 12 per MPU: no carry between the halves)
+        const int j = lane >> 3, k = lane & 7;
+        const bool cellLane = j < 7 && k < 7;
+        const uint32_t ownJK = tab->own[(j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];    // cells with i > 0
+        const uint32_t ownJK0 = tab->own[4 | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];  // the i == 0 slab
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        const int c = i * 49 + j * 7 + k;
-        const uint32_t b0 = (uint32_t)(ins[i] >> lane), b1 = (uint32_t)(ins[i + 1] >> lane);
-        uint32_t cfg = 0;
-        if (cellLane)
-            cfg = (b0 & 3u) | ((b0 >> 6) & 12u) | ((b1 & 3u) << 4) | (((b1 >> 8) & 3u) << 6);
-        uint32_t nv = 0, nt = 0;
-        if (cfg != 0 && cfg != 255) {
-            const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
-            nv = __popc(own & tab->cross[cfg]);
-            nt = tab->ntri[cfg];
+        for (int i = 0; i < 7; ++i) {
+            const int c = i * 49 + j * 7 + k;
+            const uint32_t b0 = (uint32_t)(ins[i] >> lane), b1 = (uint32_t)(ins[i + 1] >> lane);
+            uint32_t cfg = 0;
+            if (cellLane)
+                cfg = (b0 & 3u) | ((b0 >> 6) & 12u) | ((b1 & 3u) << 4) | (((b1 >> 8) & 3u) << 6);
+            uint32_t nvt = 0;
+            if (cfg != 0 && cfg != 255)
+            {
+                const uint32_t cn = tab->crossNtri[cfg];
+                nvt = (uint32_t)__popc((i == 0 ? ownJK0 : ownJK) & cn & 0xfffu) | (cn & 0xffff0000u);
+            }
+            const uint32_t svt = wave_incl_scan(nvt);  // one scan for both counts
+            if (cellLane && part == 0) {
+                const uint32_t first = carry + svt - nvt;
+                cellCfg[c] = (uint8_t)cfg;
+                cellV[c] = (uint16_t)(first & 0xffffu);
+                cellT[c] = (uint16_t)(first >> 16);
+            }
+            carry += lane_value(svt, 63);
         }
-        const uint32_t sv = wave_incl_scan(nv);
-        const uint32_t st = wave_incl_scan(nt);
-        if (cellLane) {
-            cellCfg[c] = (uint8_t)cfg;
-            cellV[c] = (uint16_t)(carryV + sv - nv);
-            cellT[c] = (uint16_t)(carryT + st - nt);
-        }
-        carryV += lane_value(sv, 63);
-        carryT += lane_value(st, 63);
-    }
-    const uint32_t V = carryV, T = carryT;
-    const uint32_t shard = (blockIdx.x * 4u + (uint32_t)wave) & (kShards - 1);
-    uint32_t qv = 0, qt = 0;
-    if (lane == 0) {
-        qv = atomicAdd(&p.ctr->shard[shard].v, V);
-        qt = atomicAdd(&p.ctr->shard[shard].t, T);
-        p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
-        if (T > 0) atomicAdd(&p.ctr->shard[shard].s, 1u);
-        if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
-    }
-    qv = lane_value(qv, 0);
-    qt = lane_value(qt, 0);
-    if (p.cull && V > 0u) {  // culling mask of the MPU box grown by the normal delta, for k_vertex
-        const float e = 7.0f * cs + 0.001f;  // and k_finish (edge samples, roots, normal samples)
-        const CullMask cg = cull_mask_box(M, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
-        if (lane == 0) {
-            p.mpuMasks[2 * w] = cg.lo;
-            p.mpuMasks[2 * w + 1] = cg.hi;
-        }
-    }
-    VertexRec* vq = p.vq + (size_t)shard * p.vShardCap;
-    TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (p.debug & 2u) return;  // ablation: pass 1 only
-
-    // pass 2 (:703-762), one lane per new vertex r: its cell is the last cell whose first
-    // vertex id is <= r; it is that cell's k-th owned crossing edge in first-occurrence
-    // order of the row, k = r - first id.  Records are written coalesced.
-    for (uint32_t base = 0; base < V; base += 64u) {
-        const uint32_t r = base + (uint32_t)lane;
-        if (r < V) {
-            const int c = find_cell(cellV, r);
-            const uint32_t cfg = cellCfg[c];
-            const int i = c / 49, j = (c / 7) % 7, k = c % 7;
-            const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
-            const uint64_t order = tab->order[cfg];
-            uint32_t left = r - cellV[c];
-            int ed = 0;
-            for (int q = 0; q < 12; ++q) {  // the (left+1)-th owned edge of the row order
-                ed = (int)((order >> (4 * q)) & 15u);
-                if ((own >> ed) & 1u) {
-                    if (left == 0u) break;
-                    --left;
+        V = carry & 0xffffu;
+        T = carry >> 16;
+        if (part == 0) {
+            const uint32_t shard = d & (kShards - 1);
+            if (lane == 0) {
+                sQ[0] = atomicAdd(&p.ctr->shard[shard].v, V);
+                sQ[1] = atomicAdd(&p.ctr->shard[shard].t, T);
+                p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
+                if (T > 0) atomicAdd(&p.ctr->shard[shard].s, 1u);
+                if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
+            }
+            if (p.cull && V > 0u) {  // culling mask of the MPU box grown by the normal delta
+                if (lane == 0) {
+                    p.mpuMasks[2 * w] = cg.lo;
+                    p.mpuMasks[2 * w + 1] = cg.hi;
                 }
             }
-            const int eb = (int)((edgeBits >> (5 * ed)) & 31u);
-            const int c1 = eb & 7, ax = eb >> 3;
-            const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
-            edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
-            const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
-            const uint32_t g = qv + r;
-            if (g < p.vShardCap) {  // pos holds the MPU origin until k_vertex writes the vertex
-                vq[g].w = w;
-                vq[g].vidKey = r | (key << 16);
-                vq[g].pos[0] = o[0];
-                vq[g].pos[1] = o[1];
-                vq[g].pos[2] = o[2];
+        }
+    }
+    phase_stamp(p, 5);
+    mpu_sync();
+    const bool recs = work && !(p.debug & 2u);  // ablation bit 1: pass 1 only
+    const uint32_t shard = d & (kShards - 1);
+    VertexRec* vq = p.vq + (size_t)shard * p.vShardCap;
+    TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
+
+    // pass 2 (:703-762), one lane per new vertex r (batches of 64 dealt to the MPU's waves
+    // in turn): its cell is the last cell whose first vertex id is <= r; it is that cell's
+    // k-th owned crossing edge in first-occurrence order of the row, k = r - first id.
+    // Records are written coalesced.
+    if (recs) {
+        const uint32_t qv = sQ[0];
+        for (uint32_t b0 = (uint32_t)part * 64u; b0 < V; b0 += 64u * kMpuWaves) {
+            const uint32_t r = b0 + (uint32_t)lane;
+            if (r < V) {
+                const int c = find_cell(cellV, r);
+                const uint32_t cfg = cellCfg[c];
+                const int i = c / 49, j = (c / 7) % 7, k = c % 7;
+                const uint32_t own = tab->own[(i == 0 ? 4 : 0) | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];
+                const uint64_t order = tab->order[cfg];
+                uint32_t left = r - cellV[c];
+                int ed = 0;
+                for (int q = 0; q < 12; ++q) {  // the (left+1)-th owned edge of the row order
+                    ed = (int)((order >> (4 * q)) & 15u);
+                    if ((own >> ed) & 1u) {
+                        if (left == 0u) break;
+                        --left;
+                    }
+                }
+                const int eb = (int)((edgeBits >> (5 * ed)) & 31u);
+                const int c1 = eb & 7, ax = eb >> 3;
+                const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
+                edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
+                const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
+                const uint32_t g = qv + r;
+                if (g < p.vShardCap) {  // pos holds the MPU origin until k_vertex writes the vertex
+                    vq[g].w = w;
+                    vq[g].vidKey = r | (key << 16);
+                    vq[g].pos[0] = o[0];
+                    vq[g].pos[1] = o[1];
+                    vq[g].pos[2] = o[2];
+                }
             }
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (p.debug & 4u) return;  // ablation: no triangles
+    phase_stamp(p, 6);
+    mpu_sync();
+    if (!recs || (p.debug & 4u)) return;  // ablation bit 2: no triangles
 
     // pass 3 (S6, :816-825), one lane per triangle r: its cell (last first-id <= r) and
     // the (r - first)-th triangle of the cell's table row
-    for (uint32_t base = 0; base < T; base += 64u) {
-        const uint32_t r = base + (uint32_t)lane;
+    const uint32_t qt = sQ[1];
+    for (uint32_t b0 = (uint32_t)part * 64u; b0 < T; b0 += 64u * kMpuWaves) {
+        const uint32_t r = b0 + (uint32_t)lane;
         if (r < T) {
             const int c = find_cell(cellT, r);
             const uint32_t t = r - cellT[c];
@@ -913,10 +1018,17 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem) {
 
 // Batches of `per` records over the kShards queues: lane l holds shard l's batch
 // count, so a batch index maps to (shard, first record) with one ballot.
+// The block's copy of the 64 shard counts of one ShardCtr field (word `field`): the first
+// 64 threads gather the 64 lines once per block; the caller syncs the block before use.
+__device__ __forceinline__ void stage_shard_counts(const Params& p, int field, uint32_t* s) {
+    if (threadIdx.x < (unsigned)kShards)
+        s[threadIdx.x] = reinterpret_cast<const uint32_t*>(&p.ctr->shard[threadIdx.x])[field];
+}
+
 struct ShardBatches {
     uint32_t cnt, incl, total;
-    __device__ ShardBatches(const uint32_t* counts, uint32_t cap, uint32_t per) {
-        cnt = min(counts[lane_id() * (sizeof(ShardCtr) / 4)], cap);  // one counter per shard line
+    __device__ ShardBatches(const uint32_t* staged, uint32_t cap, uint32_t per) {
+        cnt = min(staged[lane_id()], cap);  // staged by stage_shard_counts
         const uint32_t nb = (cnt + per - 1) / per;
         incl = wave_incl_scan(nb);
         total = lane_value(incl, kShards - 1);
@@ -1147,7 +1259,10 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const float r = (float)j * third;
     const float cs = p.cs;
     if (blockIdx.x < p.scanBlocks) scan_counts_block(p, blockIdx.x);  // block-uniform
-    const ShardBatches sb(&p.ctr->shard[0].v, p.vShardCap, 16 * VN);
+    __shared__ uint32_t sCnt[kShards];
+    stage_shard_counts(p, 1, sCnt);  // ShardCtr::v
+    __syncthreads();
+    const ShardBatches sb(sCnt, p.vShardCap, 16 * VN);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
@@ -1270,7 +1385,11 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
             }
         }
     }
-    const ShardBatches sv(&p.ctr->shard[0].v, p.vShardCap, 64);
+    __shared__ uint32_t sCnt[2 * kShards];
+    stage_shard_counts(p, 1, sCnt);            // ShardCtr::v
+    stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
+    __syncthreads();
+    const ShardBatches sv(sCnt, p.vShardCap, 64);
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
@@ -1322,7 +1441,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         }
     }
     if (p.debug & 64u) return;  // ablation bit 6: no triangles
-    const ShardBatches sb(&p.ctr->shard[0].t, p.tShardCap, 64);
+    const ShardBatches sb(sCnt + kShards, p.tShardCap, 64);
     for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
         sb.locate(batch, &shard, &first, &count);

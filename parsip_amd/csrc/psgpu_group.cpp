@@ -229,18 +229,22 @@ int psgpu_group_get_split(psgpu_group* g, uint32_t* bounds) {
 
 int psgpu_group_polygonize(psgpu_group* g, float cellsize) {
     if (!g || !g->parts[0]->haveModel || !(cellsize > 0.0f)) return PSGPU_RET_PARAM_ERROR;
-    if (g->pending) {  // the previous run's parts must finish before their buffers are reused
+    const uint32_t total = lattice_total(g, cellsize);
+    const size_t n = g->parts.size();
+    const bool replan = g->balance == PSGPU_GROUP_BALANCE_PLAN &&
+                        (!same_lattice(g, cellsize) || g->bounds.size() != n + 1 || g->bounds[n] != total);
+    if (g->pending && (replan || g->balance == PSGPU_GROUP_BALANCE_EVERY_RUN)) {
+        // the split depends on the previous run: finish it first (else runs queue up per
+        // part stream, each context double-buffers its counters)
         PsMeshInfo tmp;
         const int rc = psgpu_group_finish(g, &tmp, nullptr);
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
-    const uint32_t total = lattice_total(g, cellsize);
-    const size_t n = g->parts.size();
     if (g->balance == PSGPU_GROUP_BALANCE_FIXED) {
         if (g->bounds.size() != n + 1) even_split(g, total);
     } else if (g->balance == PSGPU_GROUP_BALANCE_EVEN) {
         even_split(g, total);
-    } else if (!same_lattice(g, cellsize) || g->bounds.size() != n + 1 || g->bounds[n] != total) {
+    } else if (replan || (g->balance == PSGPU_GROUP_BALANCE_EVERY_RUN && !same_lattice(g, cellsize))) {
         const int rc = plan(g, cellsize, total);
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <memory>
 #include <chrono>
 #include <mutex>
@@ -110,6 +111,7 @@ void fill_device_tables(const CubeTables& T, CubeTablesDev& D) {
         D.order[c] = order;
         D.cross[c] = (uint16_t)cross;
         D.ntri[c] = T.ntri[c];
+        D.crossNtri[c] = cross | ((uint32_t)T.ntri[c] << 16);
     }
     // ownership: the first cell in (i,j,k) order containing an edge owns it; an edge
     // starting at cell corner (cx,cy,cz) on axis a is owned by this cell iff every
@@ -312,24 +314,39 @@ int build_device_model(const PsSoaBlobPrims& P, const PsSoaPrimMatrices& Mx, con
         // culling skeleton (CullSeg, psgpu_model.h): a lower bound of the distance
         CullSeg& cs = D.cull[i];
         memset(&cs, 0, sizeof(cs));
+        const float inf = std::numeric_limits<float>::infinity();
+        cs.radius = inf;  // never culled unless eligible below
+        cs.tmin = 0.0f;
+        cs.tmax = 1.0f;
+        cs.axisClear = -inf;
         uint32_t flags = c ? 1u : 0u;
         if (c) {
             for (int a = 0; a < 3; ++a) cs.a[a] = d.pos[a];
+            cs.radius = 0.0f;
             double uu = 0.0;
             if (d.type == PSGPU_PRIM_LINE) {
                 for (int a = 0; a < 3; ++a) cs.u[a] = d.dir[a] - d.pos[a];
+                cs.tmin = -inf;
+                cs.tmax = inf;
                 flags |= 2u;
             } else if (d.type == PSGPU_PRIM_CYLINDER) {
                 for (int a = 0; a < 3; ++a) cs.u[a] = d.res[1] * d.dir[a];  // axis segment, length h
                 cs.radius = d.res[0];
+                cs.axisClear = 0.05f;
                 flags |= 4u;
             } else if (d.type == PSGPU_PRIM_CUBE) {
                 cs.radius = (float)(d.res[0] * 1.7320508075688772 * (1.0 + 1e-6));
             }
             for (int a = 0; a < 3; ++a) uu += (double)cs.u[a] * cs.u[a];
             cs.invUU = uu > 0.0 ? (float)(1.0 / uu) : 0.0f;
-            if (d.type == PSGPU_PRIM_CYLINDER && uu == 0.0) flags &= ~1u;  // h = 0: no axis direction
+            if (d.type == PSGPU_PRIM_CYLINDER && uu == 0.0) {  // h = 0: no axis direction
+                flags &= ~1u;
+                cs.radius = inf;
+            }
+        } else if (d.type == PSGPU_PRIM_TRIANGLE) {
+            cs.radius = -inf;  // field exactly 0 everywhere (dist2 = FLT_MAX)
         }
+        if (i >= P.ctPrims) cs.radius = inf;  // (the culling masks only cover ctPrims)
         d.cullable = flags;
     }
     // field bounds (k_precheck, prim_bound in psgpu_device.h) need every primitive the
@@ -439,6 +456,12 @@ Params make_params(psgpu_ctx* c) {
     p.preBlocks = (uint32_t)((brick_count(c) + 3) / 4);
     p.pq = c->pq;
     p.pShardCap = c->pShardCap;
+    // k_mpu: one wave per queued survivor, as many as the last finished run queued + 1/4
+    // (a run that queues more is re-run by finish(): the grid then fits exactly)
+    const uint32_t maxBlocks = (c->mpuCount + kMpusPerBlock - 1) / kMpusPerBlock;
+    const uint32_t want = c->haveQueued ? (c->lastQueued + c->lastQueued / 4 + 256 + kMpusPerBlock - 1) / kMpusPerBlock
+                                        : maxBlocks;
+    p.mpuBlocks = std::max(1u, std::min(maxBlocks, want));
     p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
     if (p.scanChunks == 0) p.scanChunks = 1;
     p.scanBlocks = (c->mpuCount + kScanItems * p.scanChunks - 1) / (kScanItems * p.scanChunks);
@@ -463,6 +486,8 @@ Params make_params(psgpu_ctx* c) {
     p.ctrNext = c->ctr + (c->parity ^ 1u);
     p.hostCtr = c->hostCtrDev;
     p.totals = c->totals;
+    p.stamps = c->stamps;
+    p.stampCap = c->stamps ? c->stampCap : 0u;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     p.debug = (uint32_t)c->debug;
     return p;
@@ -485,7 +510,7 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-    if (J) PSGPU_CHECK(launch_jit(J->mpu, kShards * ((p.pShardCap + 3) / 4), 256, mpu_lds_bytes(0), s, p));
+    if (J) PSGPU_CHECK(launch_jit(J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
@@ -518,9 +543,12 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         return PSGPU_RET_SUCCESS;
     }
     const Params p = make_params(c);
+    c->runMpuBlocks = p.mpuBlocks;
     const uint32_t slot = c->parity;
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool timed = c->timing != 0;
+    if (c->stamps)  // waves that do not run leave no stale records
+        PSGPU_CHECK(hipMemsetAsync(c->stamps, 0, (size_t)kNumStampKernels * c->stampCap * 24 + (size_t)c->stampCap * 64, s));
     if (!c->useGraph || timed || s == nullptr) {
         const int rc = launch_all(c, p, s, timed);
         if (rc != PSGPU_RET_SUCCESS) reset_run_state(c);
@@ -811,7 +839,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     drop_graphs(c);
     c->jit.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
-                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals};
+                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hostCtr) (void)hipHostFree(c->hostCtr);
@@ -857,6 +885,17 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         jit_start(c);
     }
     else if (option == PSGPU_OPT_JIT_ASYNC) c->jitAsync = value != 0;
+    else if (option == PSGPU_OPT_STAMPS && value >= 0 && value <= (1 << 24)) {
+        if (c->pending) (void)hipStreamSynchronize(c->runStream);
+        if (c->stamps) (void)hipFree(c->stamps);
+        c->stamps = nullptr;
+        c->stampCap = 0;
+        drop_graphs(c);
+        if (value > 0) {
+            PSGPU_CHECK(hipMalloc(&c->stamps, (size_t)kNumStampKernels * value * 24 + (size_t)value * 64));
+            c->stampCap = (uint32_t)value;
+        }
+    }
     else return PSGPU_RET_PARAM_ERROR;
     return PSGPU_RET_SUCCESS;
 }
@@ -923,18 +962,22 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         // grow and re-run if the work queues or the compact outputs did not fit
         for (int attempt = 0; attempt < 4; ++attempt) {
             const DevCounters& h = *c->hostCtr;
-            uint32_t V = 0, T = 0, mv = 0, mt = 0;
+            uint32_t V = 0, T = 0, mv = 0, mt = 0, Q = 0;
             for (int k = 0; k < kShards; ++k) {
                 V += h.shard[k].v;
                 T += h.shard[k].t;
+                Q += h.shard[k].p;
                 mv = std::max(mv, h.shard[k].v);
                 mt = std::max(mt, h.shard[k].t);
             }
+            const bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
+            c->lastQueued = Q;
+            c->haveQueued = c->mpuCount > 0;
             c->seenV = std::max(c->seenV, V);
             c->seenT = std::max(c->seenT, T);
             c->seenShardV = std::max(c->seenShardV, mv);
             c->seenShardT = std::max(c->seenShardT, mt);
-            if (V <= c->vcap && T <= c->tcap && mv <= c->vShardCap && mt <= c->tShardCap) break;
+            if (!gridShort && V <= c->vcap && T <= c->tcap && mv <= c->vShardCap && mt <= c->tShardCap) break;
             if (attempt == 3) return PSGPU_RET_NOT_ENOUGH_MEM;  // still short after 3 regrowths
             c->vcap = std::max(c->vcap, V + V / 8 + 1024);
             c->tcap = std::max(c->tcap, T + T / 8 + 1024);
@@ -979,6 +1022,16 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
     }
     if (!c->haveResult) return PSGPU_RET_PARAM_ERROR;
     if (info) *info = c->info;
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_download_stamps(psgpu_ctx* c, uint64_t* out, uint32_t* capOut) {
+    int rc = psgpu_finish(c, nullptr);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (capOut) *capOut = c->stamps ? c->stampCap : 0u;
+    if (!c->stamps || !out) return c->stamps ? PSGPU_RET_SUCCESS : PSGPU_RET_PARAM_ERROR;
+    PSGPU_CHECK(hipMemcpy(out, c->stamps, (size_t)kNumStampKernels * c->stampCap * 24 + (size_t)c->stampCap * 64,
+                          hipMemcpyDeviceToHost));
     return PSGPU_RET_SUCCESS;
 }
 

@@ -55,6 +55,9 @@ struct psgpu_ctx {
     size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
     uint32_t* pq = nullptr;         // sharded S1 survivor queues
     uint32_t pShardCap = 0;
+    uint32_t lastQueued = 0;        // S1 survivors queued for S2 in the last finished run
+    bool haveQueued = false;
+    uint32_t runMpuBlocks = 0;      // k_mpu grid of the last enqueued run
     uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
     uint32_t parity = 0;            // which counter / status set the next run uses
     uint64_t* counts = nullptr;
@@ -72,6 +75,8 @@ struct psgpu_ctx {
     uint32_t* tris = nullptr;
     DevCounters* ctr = nullptr;         // two sets, alternating runs
     uint32_t* totals = nullptr;         // 8 words of the last run's totals (k_finish), for RCCL
+    uint64_t* stamps = nullptr;         // per-wave timeline (PSGPU_OPT_STAMPS), 4 x stampCap x 3 words
+    uint32_t stampCap = 0;
     DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
     DevCounters* hostCtrDev = nullptr;  // its device address
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity

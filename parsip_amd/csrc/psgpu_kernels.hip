@@ -26,17 +26,17 @@ namespace psgpu {
 
 __global__ void __launch_bounds__(256) k_precheck(Params p) {
     extern __shared__ float lds[];
-    precheck_body<InterpEval>(p, lds);
+    PSGPU_STAMPED(0, item_, precheck_body<InterpEval>(p, lds));
 }
 
 __global__ void __launch_bounds__(256) k_mpu(Params p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    mpu_body<InterpEval>(p, smem);
+    PSGPU_STAMPED(1, item_, mpu_body<InterpEval>(p, smem, &item_));
 }
 
 __global__ void __launch_bounds__(256) k_vertex(Params p) {
     extern __shared__ __attribute__((aligned(16))) float vlds[];
-    vertex_body<InterpEval>(p, vlds);
+    PSGPU_STAMPED(2, item_, vertex_body<InterpEval>(p, vlds));
 }
 
 __global__ void __launch_bounds__(256) k_probe(Params p, const float* __restrict__ xyz, float* __restrict__ out,
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) k_probe(Params p, const float* __restrict
 
 __global__ void __launch_bounds__(256) k_finish(Params p) {
     extern __shared__ __attribute__((aligned(16))) float flds[];
-    finish_body<InterpEval>(p, flds);
+    PSGPU_STAMPED(3, item_, finish_body<InterpEval>(p, flds));
 }
 
 // Gathered parts of one grid (psgpu_group_gather): a part's triangles get its vertex
@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(256) k_rebase(uint32_t* __restrict__ tris, uin
 
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (psgpu_launch.h).
-size_t mpu_lds_bytes(uint32_t slots) { return kLdsTables + 4 * (kLdsSlots + (size_t)slots * 64 * 4); }
+size_t mpu_lds_bytes(uint32_t slots) { return kLdsWaveSlots + 4 * ((size_t)slots * 64 * 4); }
 size_t walk_lds_bytes(uint32_t slots) { return 4 * ((size_t)slots * 4 * 64 * 4); }
 size_t precheck_lds_bytes(uint32_t slots) { return 4 * ((size_t)slots * 64 * 4); }
 
@@ -72,8 +72,7 @@ hipError_t launch_precheck(const Params& p, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_mpu(const Params& p, hipStream_t s) {
-    const uint32_t blocks = kShards * ((p.pShardCap + 3) / 4);
-    hipLaunchKernelGGL(k_mpu, dim3(blocks), dim3(256), mpu_lds_bytes(p.slotsPerLane), s, p);
+    hipLaunchKernelGGL(k_mpu, dim3(p.mpuBlocks), dim3(256), mpu_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
 hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks) {

@@ -56,6 +56,8 @@ namespace psgpu {
 //   ntri[c]  triangles in the row
 //   own[b]   12-bit mask of edges a cell owns, b = (i==0)<<2 | (j==0)<<1 | (k==0)
 //   edge     per edge: corner1 (3 bits) | axis << 3, 5 bits per edge
+//   crossNtri[c] cross[c] | ntri[c] << 16 (pass 1's one lookup per cell)
+// k_mpu reads them from global memory (the 5.9 KB stay in every CU's L1 / L2).
 struct CubeTablesDev {
     uint64_t row[256];
     uint64_t order[256];
@@ -64,6 +66,7 @@ struct CubeTablesDev {
     uint16_t own[8];
     uint64_t edge;
     uint8_t pad[8];
+    uint32_t crossNtri[256];
 };
 
 enum InstrKind : uint8_t { kEnter = 0, kPrim = 1, kOp = 2, kSumPrim = 3 };
@@ -107,15 +110,21 @@ static_assert(sizeof(DevPrim) == 128, "DevPrim size");
 constexpr int kMaxInstr = 512;
 constexpr int kMaxSlots = 64;
 
-// Culling skeleton of a primitive: the segment A + t*U (t in [0,1], or any t for the
-// unbounded Line) whose distance minus cullRadius bounds the primitive's distance
-// from below; one branch-free formula for every type.
-struct CullSeg {         // 32 B
+// Culling skeleton of a primitive: the segment A + t*U, t in [tmin, tmax] ([0,1]; any t
+// for the unbounded Line), whose distance minus `radius` bounds the primitive's distance
+// from below; one branch-free formula for every slot: radius = +inf never culls (not
+// eligible, or past ctPrims), -inf always culls (Triangle: field exactly 0).
+struct CullSeg {         // 48 B: three 16-B loads per lane
     float a[3];
     float u[3];
     float invUU;         // 1 / |U|^2, 0 for a point
     float radius;
+    float tmin, tmax;
+    float axisClear;     // the box must keep this distance from the segment's line (Cylinder: its
+                         // rounded-negative sqrt is NaN on the axis); -inf: no condition
+    float pad;
 };
+static_assert(sizeof(CullSeg) == 48, "CullSeg size");
 
 struct DevModel {
     uint32_t nInstr;
@@ -167,6 +176,16 @@ struct DevCounters {
     ShardCtr shard[kShards];
 };
 
+#ifndef PSGPU_MPU_WAVES
+#define PSGPU_MPU_WAVES 2  // waves per S1 survivor in k_mpu (1, 2 or 4): each walks 8 / W of the
+                           // 8 x-slices of the S2 cache and takes every W-th batch of records,
+                           // so a heavy MPU's critical path is ~1/W of one wave doing it all.
+                           // Host and device must agree (build.py and the JIT pass the same value).
+#endif
+constexpr int kMpuWaves = PSGPU_MPU_WAVES;
+constexpr int kMpusPerBlock = 4 / kMpuWaves;  // k_mpu blocks are 4 waves
+constexpr int kNumStampKernels = 4;  // k_precheck, k_mpu, k_vertex, k_finish
+
 // Kernel arguments of one polygonization (one struct, passed by value).
 struct Params {
     const DevModel* __restrict__ model;
@@ -183,6 +202,7 @@ struct Params {
     uint32_t brickDims[3];  // bricks of the range along x, y, z
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
+    uint32_t mpuBlocks;     // k_mpu grid (4 waves per block, kMpusPerBlock queued survivors per block)
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
     uint8_t* passed;        // mpuCount: 1 if the MPU passed S1 (PsMpuStats::passedPrecheck)
     uint32_t bound;         // k_precheck proves S1 survivors empty by field bounds
@@ -206,6 +226,8 @@ struct Params {
     DevCounters* hostCtr;   // host-mapped copy written by k_finish
     uint32_t* totals;       // 8 words written by k_finish: MPUs, V, T, passed S1, surface MPUs,
                             // S2 MPUs, first overflow MPU, error (the parts' count exchange)
+    uint64_t* stamps;       // per-wave timeline (PSGPU_OPT_STAMPS) or null: kNumStampKernels x
+    uint32_t stampCap;      // stampCap records {start, end, item | hw id << 32} (s_memrealtime)
     uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
     uint32_t debug;         // ablation switches for profiling (0 in production)
 };

@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_group_get_split", "psgpu_group_polygonize", "psgpu_group_finish", "psgpu_group_download_mesh",
     "psgpu_group_gather", "psgpu_group_export_polympus", "psgpu_group_polygonize_mpus",
     "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
-    "psgpu_comm_result",
+    "psgpu_comm_result", "psgpu_download_stamps",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -69,6 +69,8 @@ OPT_CAPACITY = 6
 OPT_GRAPH = 7
 OPT_BOUND = 10
 OPT_JIT_ASYNC = 11
+OPT_STAMPS = 12
+STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
 BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3
 COMM_ID_BYTES = 128
@@ -111,6 +113,7 @@ def load(build_if_missing: bool = True):
         "psgpu_jit_source": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "psgpu_jit_compile": ([vp, vp, vp, i32, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
         "psgpu_mpu_costs": ([vp, vp], i32),
+        "psgpu_download_stamps": ([vp, vp, ctypes.POINTER(u32)], i32),
         "psgpu_split_costs": ([vp, u32, u32, u32, vp], i32),
         "psgpu_group_create": ([vp, i32, ctypes.POINTER(vp)], i32),
         "psgpu_group_destroy": ([vp], None),
@@ -324,6 +327,19 @@ class Polygonizer:
         context (deterministic: every rank computes the same split)."""
         self.run(cellsize)
         return split_costs(self.mpu_costs(), parts)
+
+    def stamps(self) -> dict:
+        """Per-wave timeline of the last run (OPT_STAMPS): kernel -> (waves, 3) uint64 array
+        of start, end (100 MHz ticks), item | hw id << 32, launched waves only."""
+        cap = ctypes.c_uint32()
+        _check(self._L.psgpu_download_stamps(self._ctx, None, ctypes.byref(cap)), "psgpu_download_stamps")
+        n = max(cap.value, 1)
+        raw = np.zeros(len(STAMP_KERNELS) * n * 3 + n * 8, np.uint64)
+        _check(self._L.psgpu_download_stamps(self._ctx, raw.ctypes.data, ctypes.byref(cap)), "psgpu_download_stamps")
+        buf = raw[:len(STAMP_KERNELS) * n * 3].reshape(len(STAMP_KERNELS), n, 3)
+        out = {k: buf[i][buf[i][:, 0] != 0] for i, k in enumerate(STAMP_KERNELS)}
+        out["mpu_phases"] = raw[len(STAMP_KERNELS) * n * 3:].reshape(n, 8)
+        return out
 
     def kernel_times(self) -> dict:
         ms = (ctypes.c_float * 8)()

@@ -1,0 +1,123 @@
+"""Per-wave timeline of one polygonization (PSGPU_OPT_STAMPS, s_memrealtime at 100 MHz).
+
+usage: python tools/timeline.py [--config C3] [--jit 1] [--json out.json]
+Prints, per kernel: waves, span (first start -> last end), the gap after the previous
+kernel, wave lifetime percentiles, the share of the span during which fewer than 1/4 of
+the peak number of waves were running (the tail), and a 20-bin profile of running waves.
+For k_mpu, waves that polygonized an MPU and empty waves are reported apart.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from parsip_amd import gpu, synth  # noqa: E402
+
+TICK_US = 0.01  # 100 MHz
+
+
+def profile(st, t0, t1, bins=20):
+    edges = np.linspace(t0, t1, bins + 1)
+    mids = 0.5 * (edges[:-1] + edges[1:])
+    return [int(np.count_nonzero((st[:, 0] <= m) & (st[:, 1] >= m))) for m in mids]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--jit", type=int, default=1)
+    ap.add_argument("--runs", type=int, default=5)
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    model, cs, N = synth.make_config(a.config)
+    p = gpu.Polygonizer(0)
+    p.set_option(gpu.OPT_JIT, a.jit)
+    p.set_model(model)
+    for _ in range(3):
+        p.run(cs)
+    p.set_option(gpu.OPT_STAMPS, 1 << 17)
+    report = {}
+    for run in range(a.runs):
+        p.run(cs)
+        S = p.stamps()
+    prev_end = None
+    first = min(int(S[k][:, 0].min()) for k in gpu.STAMP_KERNELS if len(S[k]))
+    for k in gpu.STAMP_KERNELS:
+        st = S[k].astype(np.int64)
+        if not len(st):
+            continue
+        t0, t1 = int(st[:, 0].min()), int(st[:, 1].max())
+        life = (st[:, 1] - st[:, 0]) * TICK_US
+        prof = profile(st, t0, t1)
+        peak = max(prof)
+        tail = sum(1 for x in prof if x < peak / 4) / len(prof)
+        e = {"waves": int(len(st)), "start_us": round((t0 - first) * TICK_US, 2), "span_us": round((t1 - t0) * TICK_US, 2),
+             "gap_before_us": None if prev_end is None else round((t0 - prev_end) * TICK_US, 2),
+             "life_us_p50": round(float(np.percentile(life, 50)), 2),
+             "life_us_p90": round(float(np.percentile(life, 90)), 2), "life_us_max": round(float(life.max()), 2),
+             "last_start_us": round((int(st[:, 0].max()) - t0) * TICK_US, 2),
+             "tail_share": round(tail, 2), "running_waves_20bins": prof}
+        if k == "k_mpu":
+            item = (st[:, 2] & 0xFFFFFFFF).astype(np.int64)
+            real = item != 0xFFFFFFFF
+            e["real_waves"] = int(real.sum())
+            e["real_life_us_p50"] = round(float(np.percentile(life[real], 50)), 2) if real.any() else None
+            e["real_life_us_max"] = round(float(life[real].max()), 2) if real.any() else None
+            e["empty_life_us_p50"] = round(float(np.percentile(life[~real], 50)), 2) if (~real).any() else None
+        report[k] = e
+        prev_end = t1
+        print(f"{k:10s} waves={e['waves']:6d} start={e['start_us']:7.2f} span={e['span_us']:6.2f}us "
+              f"gap={e['gap_before_us']} life p50/p90/max={e['life_us_p50']}/{e['life_us_p90']}/{e['life_us_max']} "
+              f"last_start={e['last_start_us']} tail={e['tail_share']}")
+        print(f"{'':10s} running: {prof}")
+        if k == "k_mpu":
+            print(f"{'':10s} real waves={e['real_waves']} life p50/max={e['real_life_us_p50']}/{e['real_life_us_max']} "
+                  f"empty p50={e['empty_life_us_p50']}")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(report, f, indent=1)
+
+
+
+
+def mpu_phases(config="C3"):
+    """k_mpu phase stamps (debug bit 4096): per real wave, the time spent between entry,
+    table staging, MPU fetch + cull mask, S2 walk, the inside-bit barrier, pass 1 (+barrier),
+    pass 2 (+barrier) and the end (the k_mpu record's end stamp)."""
+    model, cs, N = synth.make_config(config)
+    p = gpu.Polygonizer(0)
+    p.set_model(model)
+    for _ in range(3):
+        p.run(cs)
+    p.set_option(gpu.OPT_STAMPS, 1 << 17)
+    p.set_option(gpu.OPT_DEBUG, 4096)
+    p.run(cs)
+    S = p.stamps()
+    ph = S["mpu_phases"].astype(np.int64)
+    rec = S["k_mpu"].astype(np.int64)
+    n = len(rec)
+    ph = ph[:n]
+    item = (rec[:, 2] & 0xFFFFFFFF)
+    real = (item != 0xFFFFFFFF) & (ph[:, 3] != 0)
+    t0 = rec[:, 0].min()
+    names = ["stage tables", "fetch+cullmask", "S2 walk", "ins barrier", "pass 1", "pass 2", "pass 3+end"]
+    cols = [ph[:, 0], ph[:, 1], ph[:, 2], ph[:, 3], ph[:, 4], ph[:, 5], ph[:, 6], rec[:, 1]]
+    print(f"k_mpu real waves {int(real.sum())} of {n}")
+    for i, nm in enumerate(names):
+        a, b = cols[i][real], cols[i + 1][real]
+        ok = (a > 0) & (b > 0)
+        dt = (b[ok] - a[ok]) * TICK_US
+        if len(dt):
+            print(f"  {nm:15s} median {np.median(dt):6.2f} us  p90 {np.percentile(dt, 90):6.2f}  max {dt.max():6.2f}")
+    st = (ph[real, 0] - t0) * TICK_US
+    print(f"  wave entry time: median {np.median(st):.2f} us, p90 {np.percentile(st, 90):.2f}, max {st.max():.2f}")
+
+
+if __name__ == "__main__":
+    if "--phases" in sys.argv:
+        mpu_phases()
+    else:
+        main()
