@@ -186,6 +186,9 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="N>1: strong (default: one grid split over the ranks) or weak (a grid per rank)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="per device: the rank's MPU range as this many cost-balanced parts on as many HIP "
+                         "streams (their kernels overlap each other's tails); 1 = one context")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
@@ -223,27 +226,50 @@ def main():
 
     comm, exchange = None, None
     full = None
-    if scaling == "strong" and grp.world > 1:
-        bounds = poly.plan_split(cs, grp.world)  # one full run; the same split on every rank
+    # the cost split: one full planning run on this rank's device (exact results, so every
+    # rank computes the same split without communication)
+    strong = scaling == "strong" and grp.world > 1
+    nstreams = max(1, args.streams)
+    costs = None
+    if strong or nstreams > 1:
+        poly.run(cs)
         full = poly.finish()
+        costs = poly.mpu_costs()
+    if strong:
+        bounds = gpu.split_costs(costs, grp.world)
         begin, end = int(bounds[grp.rank]), int(bounds[grp.rank + 1])
+    else:
+        begin, end = 0, n_mpus
+        full = None
+    eng = poly
+    if nstreams > 1:  # the rank's range as `parts` cost-balanced sub-ranges, one stream each
+        eng = gpu.Group([device] * nstreams)
+        if args.no_cull:
+            eng.set_option(gpu.OPT_CULLING, 0)
+        eng.set_option(gpu.OPT_JIT, args.jit)
+        eng.set_model(model)
+        eng.set_split(gpu.split_costs(costs[begin:end], nstreams, begin))
+    if strong:
         if pinned is None:
             uid = grp.broadcast_bytes(gpu.comm_unique_id() if grp.rank == 0 else None)
-            comm = gpu.Comm(poly, uid, grp.world, grp.rank)
+            comm = gpu.Comm(eng, uid, grp.world, grp.rank)
             exchange = "rccl all-gather of 8 words per rank per step (library stream)"
         else:
             exchange = "gloo all-gather after the timed steps (ranks share one device: RCCL needs distinct GPUs)"
-    else:
-        begin, end = 0, n_mpus
 
     def step():
-        poly.polygonize(cs, begin, end)
+        if nstreams > 1:
+            eng.polygonize(cs)
+        else:
+            poly.polygonize(cs, begin, end)
         if comm:
             comm.exchange()
 
     def finish():
         if comm:
             return comm.result()
+        if nstreams > 1:
+            return eng.finish()
         return poly.finish(), None
 
     for _ in range(args.warmup):
@@ -253,7 +279,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    info, parts = finish()
+    info, _ = finish()
     grp.barrier()
     t1 = time.perf_counter()
     dt = grp.max(t1 - t0)
@@ -261,7 +287,7 @@ def main():
     cells_per_step = N ** 3 * (grp.world if scaling == "weak" else 1)
     value = cells_per_step / (ms_step * 1e-3) / 1e6
 
-    mine = poly.finish()
+    mine = eng.finish()[0] if nstreams > 1 else poly.finish()
     counts = grp.allgather([mine.ctMPUs, mine.ctVertices, mine.ctTriangles])
     check = None
     if full is not None:  # the parts must add up to the full grid of the planning run
@@ -273,7 +299,8 @@ def main():
         if not ok:
             sys.exit(f"bench.py rank {grp.rank}: parts {counts} do not add up to the full grid {check['full']}")
 
-    # roofline pass: per-kernel hipEvent timing on the library's stream
+    # roofline pass: per-kernel hipEvent timing on the library's stream, one context over
+    # the rank's whole range (single stream: per-launch figures comparable with rocprof)
     poly.set_option(gpu.OPT_KERNEL_TIMING, 1)
     kt = {}
     reps = max(3, min(args.steps, 20))
@@ -282,16 +309,17 @@ def main():
         for k, v in poly.kernel_times().items():
             kt[k] = kt.get(k, 0.0) + v / reps
     poly.set_option(gpu.OPT_KERNEL_TIMING, 0)
+    single = poly.finish()  # the counts of that single-stream run
     dom = max(kt, key=kt.get)
     # lane-evaluations each launch processes (SURVEY.md §8(d) units) ...
-    launch_evals = {"k_precheck": 8 * mine.ctMPUs, "k_mpu": 512 * mine.ctFieldMPUs,
-                    "k_vertex": 4 * mine.ctVertices, "k_finish": 4 * mine.ctVertices}
+    launch_evals = {"k_precheck": 8 * single.ctMPUs, "k_mpu": 512 * single.ctFieldMPUs,
+                    "k_vertex": 4 * single.ctVertices, "k_finish": 4 * single.ctVertices}
     # ... times the fp32 ops per lane-evaluation of that stage that the reference executes on
     # this input (its own op-box pruning included; the oracle's counters priced by
     # parsip_amd/costmodel.py, tests/golden/workload_ops.json); else the unpruned figure
     wops = workload_ops(args.config) if scaling == "weak" or grp.world == 1 else None
     per_eval, per_src = costmodel.ops_per_eval(model), "costmodel.ops_per_eval (unpruned tree)"
-    if wops and wops.get("vertices") == mine.ctVertices and dom in wops:
+    if wops and wops.get("vertices") == single.ctVertices and dom in wops:
         ref_evals = {"k_precheck": 8 * mine.ctMPUs, "k_mpu": 512 * wops["passed_s1"],
                      "k_vertex": 4 * wops["vertices"], "k_finish": 4 * wops["vertices"]}[dom]
         per_eval, per_src = wops[dom] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
@@ -309,8 +337,9 @@ def main():
             "kernel_ms": round(kt[dom], 4), "lane_evals": launch_evals[dom], "ops_per_eval": round(per_eval, 1),
             "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
             "note": "achieved = lane-evaluations this launch performs x the reference's fp32 ops per "
-                    "evaluation / hipEvent launch time; exact per-wave culling skips part of those ops, so "
-                    "valu_issue (executed VALU instructions x 2 cycles per wave64 on SIMD-32, PMC) is the "
+                    "evaluation / hipEvent launch time, on a single-stream run of the rank's whole range (the "
+                    "timed steps run it as `streams` parts); exact per-wave culling skips part of those ops, "
+                    "so valu_issue (executed VALU instructions x 2 cycles per wave64 on SIMD-32, PMC) is the "
                     "hardware-side utilisation"}
     if pe and "SQ_INSTS_VALU" in pe:
         roof["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (kt[dom] * 1e-3 * 2.4e9 * 1024), 4)
@@ -336,7 +365,8 @@ def main():
                                + (" split over the ranks (C4)" if full is not None else "")
                                + (", a grid per rank (frame = rank)" if scaling == "weak" and grp.world > 1 else ""),
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,
-                   "parallelism": f"{scaling}-{grp.world}gpu", "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
+                   "parallelism": f"{scaling}-{grp.world}gpu", "streams_per_gpu": nstreams,
+                   "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
                    "exchange": exchange, "culling": not args.no_cull,
                    "kernels": ["interpreter", "jit-structure", "jit-baked"][args.jit] if jit_on or args.jit == 0
                    else "interpreter (jit unavailable)", "set_model_s": round(t_model, 4),
@@ -355,6 +385,8 @@ def main():
         print(json.dumps(out), flush=True)
     if comm:
         comm.close()
+    if nstreams > 1:
+        eng.close()
     if grp.dist:
         grp.dist.destroy_process_group()
     poly.close()

@@ -336,6 +336,9 @@ int  psgpu_comm_create(psgpu_ctx* ctx, const uint8_t id[PSGPU_COMM_ID_BYTES], in
 void psgpu_comm_destroy(psgpu_comm* comm);
 /* Enqueue the all-gather of the context's last polygonization (after psgpu_polygonize). */
 int  psgpu_comm_exchange(psgpu_comm* comm, psgpu_ctx* ctx);
+/* The same for a rank whose range runs as a group of parts on its one device (several
+ * streams): their totals are summed on part 0's stream before the all-gather. */
+int  psgpu_comm_exchange_group(psgpu_comm* comm, psgpu_group* g);
 /* Wait; totals over all ranks and, if parts != NULL, nranks entries (rank order). */
 int  psgpu_comm_result(psgpu_comm* comm, PsMeshInfo* total, PsGroupPart* parts);
 

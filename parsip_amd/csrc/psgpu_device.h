@@ -732,6 +732,28 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(queue8));
     base = lane_value(base, 0);
     if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u))] = mOf;
+    // Culling masks of each queued MPU, from this wave's culling segments (already in
+    // registers): its box for S2 (with the queue entry: k_mpu loads no culling data) and the
+    // box grown by the normal delta for k_vertex / k_finish
+    if (p.cull) {
+        const float e = 7.0f * p.cs, eg = 7.0f * p.cs + 0.001f;
+        for (uint32_t qm = queue8; qm != 0u; qm &= qm - 1u) {
+            const int q = __builtin_ctz(qm);
+            const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[0]), 8 * q));
+            const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[1]), 8 * q));
+            const float oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[2]), 8 * q));
+            const CullMask a = cull_mask_from(cl, ox, oy, oz, ox + e, oy + e, oz + e);
+            const CullMask g = cull_mask_from(cl, ox, oy, oz, ox + eg, oy + eg, oz + eg);
+            const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << q) - 1u));
+            const uint32_t wq = lane_value(mOf, q) - p.mpuBegin;
+            if (lane == 0) {
+                p.pqMask[2 * slotq] = a.lo;
+                p.pqMask[2 * slotq + 1] = a.hi;
+                p.mpuMasks[2 * wq] = g.lo;
+                p.mpuMasks[2 * wq + 1] = g.hi;
+            }
+        }
+    }
 }
 
 #ifndef PSGPU_S2_N
@@ -795,14 +817,12 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     ModelPtr M = as_const(p.model);
     const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
     // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
-    // the block; every lane meanwhile loads its culling segments
+    // the block
     __shared__ uint32_t sIncl[kShards];
     if (wave == 0) {
         const uint32_t cnt = p.ctr->shard[lane].p;  // kShards == 64: one shard per lane
         sIncl[lane] = wave_incl_scan(cnt);
     }
-    CullLanes cl;
-    if (p.cull) cl = load_cull_lanes(M);
     __syncthreads();
     // MPU d = block * (4 / W) + slot is the d-th queued survivor in shard order (dense over
     // the 64 shard queues); the grid is sized by the host from the last finished run, and
@@ -813,10 +833,16 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     const bool live = d < pcount;
     uint32_t m = 0, w = 0;
     float o[3] = {0.0f, 0.0f, 0.0f};
+    CullMask cm{0ull, 0ull};
     if (live) {
         const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
         const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
-        m = __builtin_amdgcn_readfirstlane(p.pq[pshard * p.pShardCap + pidx]);
+        const uint32_t slotq = pshard * p.pShardCap + pidx;
+        m = __builtin_amdgcn_readfirstlane(p.pq[slotq]);
+        if (p.cull) {  // the MPU box's culling mask, made by k_precheck
+            cm.lo = p.pqMask[2 * slotq];
+            cm.hi = p.pqMask[2 * slotq + 1];
+        }
         *item = m;
         w = m - p.mpuBegin;  // slot of the MPU in the range: counts / offsets index
         mpu_origin(p, m, o);
@@ -833,21 +859,12 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     EV ev(M, reinterpret_cast<float*>(smem + kLdsWaveSlots + wave * p.slotsPerLane * 64 * 4) + lane);
     const float cs = p.cs;
 
-    CullMask cm{0ull, 0ull}, cg{0ull, 0ull};
     if (live) {
         // S2 (:550-610): corner (x, y, z) of the 8x8x8 cache, lane = y*8 + z, this wave's
         // NX x-slices per lane; quads = 4 consecutive z
         const int y = lane >> 3, z = lane & 7;
         const float py = o[1] + (float)y * cs;
         const float pz = o[2] + (float)z * cs;
-        if (p.cull) {
-            const float e = 7.0f * cs;
-            cm = cull_mask_from(cl, o[0], o[1], o[2], o[0] + e, o[1] + e, o[2] + e);
-            // the MPU box grown by the normal delta, for k_vertex and k_finish (edge samples,
-            // roots, normal samples), stored by the first wave if the MPU has vertices
-            const float eg = 7.0f * cs + 0.001f;
-            if (part == 0) cg = cull_mask_from(cl, o[0], o[1], o[2], o[0] + eg, o[1] + eg, o[2] + eg);
-        }
         phase_stamp(p, 2);
         float pxs[NX], pys[NX], pzs[NX], fs[NX];
 #pragma unroll
@@ -932,12 +949,6 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
                 p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
                 if (T > 0) atomicAdd(&p.ctr->shard[shard].s, 1u);
                 if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
-            }
-            if (p.cull && V > 0u) {  // culling mask of the MPU box grown by the normal delta
-                if (lane == 0) {
-                    p.mpuMasks[2 * w] = cg.lo;
-                    p.mpuMasks[2 * w + 1] = cg.hi;
-                }
             }
         }
     }

@@ -51,6 +51,9 @@ struct psgpu_group {
     uint32_t* gTris = nullptr;
     uint64_t* gOffs = nullptr;
     size_t gCapV = 0, gCapT = 0, gCapM = 0;
+    // one rank's parts summed for the RCCL exchange (psgpu_comm_exchange_group)
+    std::vector<hipEvent_t> done;
+    uint32_t* sumTotals = nullptr;
 };
 
 namespace {
@@ -166,6 +169,10 @@ int psgpu_group_create(const int* devices, int nParts, psgpu_group** out) {
 void psgpu_group_destroy(psgpu_group* g) {
     if (!g) return;
     free_gather(g);
+    if (!g->parts.empty()) (void)hipSetDevice(g->parts[0]->device);
+    for (hipEvent_t e : g->done)
+        if (e) (void)hipEventDestroy(e);
+    if (g->sumTotals) (void)hipFree(g->sumTotals);
     for (psgpu_ctx* c : g->parts) psgpu_destroy(c);
     delete g;
 }
@@ -443,6 +450,7 @@ struct psgpu_comm {
     uint32_t* hostGathered = nullptr;  // pinned copy
     bool pending = false;
     psgpu_ctx* ctx = nullptr;          // the context whose run was exchanged
+    psgpu_group* group = nullptr;      // or the group whose parts were summed
 };
 
 static int nccl_fail(ncclResult_t r, const char* what) {
@@ -507,6 +515,47 @@ int psgpu_comm_exchange(psgpu_comm* m, psgpu_ctx* ctx) {
                                hipMemcpyDeviceToHost, s));
     m->pending = true;
     m->ctx = ctx;
+    m->group = nullptr;
+    return PSGPU_RET_SUCCESS;
+}
+
+// The same for a rank whose range runs as a group of parts on its one device (several
+// streams): part 0's stream waits for the others' last launches, sums their totals and
+// all-gathers the sum.
+int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
+    if (!m || !g || g->parts.empty() || g->parts.size() > 16) return PSGPU_RET_PARAM_ERROR;
+    for (psgpu_ctx* c : g->parts)
+        if (c->device != m->device) return PSGPU_RET_PARAM_ERROR;
+    psgpu_ctx* c0 = g->parts[0];
+    int rc = set_device(c0);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (g->done.size() != g->parts.size()) {
+        for (hipEvent_t e : g->done)
+            if (e) (void)hipEventDestroy(e);
+        g->done.assign(g->parts.size(), nullptr);
+        for (hipEvent_t& e : g->done) PSGPU_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (!g->sumTotals) PSGPU_CHECK(hipMalloc(&g->sumTotals, 8 * sizeof(uint32_t)));
+    hipStream_t s0 = c0->runStream ? c0->runStream : c0->stream;
+    TotalsParts tp{};
+    tp.n = (int)g->parts.size();
+    for (size_t k = 0; k < g->parts.size(); ++k) {
+        psgpu_ctx* c = g->parts[k];
+        tp.p[k] = c->totals;
+        hipStream_t sk = c->runStream ? c->runStream : c->stream;
+        if (sk != s0) {
+            PSGPU_CHECK(hipEventRecord(g->done[k], sk));
+            PSGPU_CHECK(hipStreamWaitEvent(s0, g->done[k], 0));
+        }
+    }
+    PSGPU_CHECK(launch_sum_totals(tp, g->sumTotals, s0));
+    rc = nccl_fail(ncclAllGather(g->sumTotals, m->gathered, 8, ncclUint32, m->comm, s0), "ncclAllGather");
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, (size_t)m->nranks * 8 * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s0));
+    m->pending = true;
+    m->ctx = c0;
+    m->group = g;
     return PSGPU_RET_SUCCESS;
 }
 
@@ -517,14 +566,14 @@ int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut
     if (!m || !m->pending || !m->ctx) return PSGPU_RET_PARAM_ERROR;
     psgpu_ctx* c = m->ctx;
     PsMeshInfo mine;
-    int rc = psgpu_finish(c, &mine);
+    int rc = m->group ? psgpu_group_finish(m->group, &mine, nullptr) : psgpu_finish(c, &mine);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     hipStream_t s = c->runStream ? c->runStream : c->stream;
     PSGPU_CHECK(hipStreamSynchronize(s));
     const uint32_t* mineG = m->hostGathered + 8 * m->rank;
-    if (c->mpuCount && (mineG[1] != mine.ctVertices || mineG[2] != mine.ctTriangles)) {
+    if (mine.ctMPUs && (mineG[1] != mine.ctVertices || mineG[2] != mine.ctTriangles)) {
         // finish() re-ran the polygonization with grown buffers: exchange its totals
-        rc = psgpu_comm_exchange(m, c);
+        rc = m->group ? psgpu_comm_exchange_group(m, m->group) : psgpu_comm_exchange(m, c);
         if (rc != PSGPU_RET_SUCCESS) return rc;
         PSGPU_CHECK(hipStreamSynchronize(s));
     }

@@ -424,6 +424,7 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     const size_t n = std::max<uint32_t>(mpuCount, 1);
     c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
     PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
+    PSGPU_CHECK(grow(c->pqMask, c->capPqMask, (size_t)c->pShardCap * kShards * 2));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
     PSGPU_CHECK(grow(c->passed, c->capPassed, n));
     PSGPU_CHECK(grow(c->mpuMasks, c->capMasks, 2 * n));
@@ -455,6 +456,7 @@ Params make_params(psgpu_ctx* c) {
     brick_layout(c, &p.brickI0, p.brickDims);
     p.preBlocks = (uint32_t)((brick_count(c) + 3) / 4);
     p.pq = c->pq;
+    p.pqMask = c->pqMask;
     p.pShardCap = c->pShardCap;
     // k_mpu: one wave per queued survivor, as many as the last finished run queued + 1/4
     // (a run that queues more is re-run by finish(): the grid then fits exactly)
@@ -838,7 +840,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graphs(c);
     c->jit.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->pq, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps};
     for (void* b : bufs)
         if (b) (void)hipFree(b);

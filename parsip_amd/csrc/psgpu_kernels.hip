@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "psgpu_device.h"
+#include "psgpu_launch.h"
 
 namespace psgpu {
 
@@ -61,6 +62,21 @@ __global__ void __launch_bounds__(256) k_rebase(uint32_t* __restrict__ tris, uin
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nOff; i += stride) offs[i] += offBase;
 }
 
+// The totals of a rank's parts (one device, several streams) as one rank's 8 words for
+// the RCCL exchange: counts add, the first overflowing MPU is the minimum, errors OR.
+__global__ void __launch_bounds__(64) k_sum_totals(TotalsParts tp, uint32_t* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i >= 8) return;
+    uint32_t v = i == 6 ? 0x7fffffffu : 0u;
+    for (int k = 0; k < tp.n; ++k) {
+        const uint32_t x = tp.p[k][i];
+        if (i == 6) v = x < v ? x : v;
+        else if (i == 7) v |= x;
+        else v += x;
+    }
+    out[i] = v;
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (psgpu_launch.h).
 size_t mpu_lds_bytes(uint32_t slots) { return kLdsWaveSlots + 4 * ((size_t)slots * 64 * 4); }
@@ -98,6 +114,11 @@ hipError_t launch_rebase(uint32_t* tris, uint64_t nTri, uint32_t vBase, uint64_t
     uint64_t blocks = (n + 1023) / 1024;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(k_rebase, dim3((uint32_t)blocks), dim3(256), 0, s, tris, nTri, vBase, offs, nOff, offBase);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_totals(const TotalsParts& tp, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_totals, dim3(1), dim3(64), 0, s, tp, out);
     return hipGetLastError();
 }
 

@@ -201,12 +201,13 @@ struct Params {
     uint32_t brickI0;       // first brick row (x) touching the MPU range
     uint32_t brickDims[3];  // bricks of the range along x, y, z
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
+    uint64_t* pqMask;       // per queue entry: the MPU box's culling mask (2 words, by k_precheck)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
     uint32_t mpuBlocks;     // k_mpu grid (4 waves per block, kMpusPerBlock queued survivors per block)
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
     uint8_t* passed;        // mpuCount: 1 if the MPU passed S1 (PsMpuStats::passedPrecheck)
     uint32_t bound;         // k_precheck proves S1 survivors empty by field bounds
-    uint64_t* mpuMasks;     // 2 * mpuCount: culling mask of each surface MPU's box + delta
+    uint64_t* mpuMasks;     // 2 * mpuCount: culling mask of each queued MPU's box + delta (k_precheck)
     uint64_t* offs;         // mpuCount + 1: exclusive scan of counts
     uint64_t* scanStatus;   // offsets-scan look-back words of this run (zeroed by the previous run)
     uint64_t* scanStatusNext;

@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_group_get_split", "psgpu_group_polygonize", "psgpu_group_finish", "psgpu_group_download_mesh",
     "psgpu_group_gather", "psgpu_group_export_polympus", "psgpu_group_polygonize_mpus",
     "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
-    "psgpu_comm_result", "psgpu_download_stamps",
+    "psgpu_comm_result", "psgpu_download_stamps", "psgpu_comm_exchange_group",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -134,6 +134,7 @@ def load(build_if_missing: bool = True):
         "psgpu_comm_create": ([vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
         "psgpu_comm_destroy": ([vp], None),
         "psgpu_comm_exchange": ([vp, vp], i32),
+        "psgpu_comm_exchange_group": ([vp, vp], i32),
         "psgpu_comm_result": ([vp, ctypes.POINTER(PsMeshInfo), vp], i32),
     }
     for name, (args, res) in sig.items():
@@ -478,14 +479,17 @@ def comm_unique_id() -> bytes:
 class Comm:
     """RCCL count exchange of one rank's polygonization (one process per GPU)."""
 
-    def __init__(self, poly: Polygonizer, uid: bytes, nranks: int, rank: int):
+    def __init__(self, poly, uid: bytes, nranks: int, rank: int):
+        """poly: the rank's Polygonizer, or a Group of parts on the rank's one device."""
         assert len(uid) == COMM_ID_BYTES
         self._L = load()
         self._poly = poly
+        self._group = poly if isinstance(poly, Group) else None
+        ctx = ctypes.c_void_p(poly.context_ptr(0)) if self._group else poly._ctx
         self.nranks = nranks
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
         self._c = ctypes.c_void_p()
-        _check(self._L.psgpu_comm_create(poly._ctx, buf, nranks, rank, ctypes.byref(self._c)), "psgpu_comm_create")
+        _check(self._L.psgpu_comm_create(ctx, buf, nranks, rank, ctypes.byref(self._c)), "psgpu_comm_create")
 
     def close(self):
         if getattr(self, "_c", None) and self._c.value:
@@ -495,7 +499,10 @@ class Comm:
     __del__ = close
 
     def exchange(self) -> None:
-        _check(self._L.psgpu_comm_exchange(self._c, self._poly._ctx), "psgpu_comm_exchange")
+        if self._group:
+            _check(self._L.psgpu_comm_exchange_group(self._c, self._group._g), "psgpu_comm_exchange_group")
+        else:
+            _check(self._L.psgpu_comm_exchange(self._c, self._poly._ctx), "psgpu_comm_exchange")
 
     def result(self):
         info = PsMeshInfo()
