@@ -184,6 +184,8 @@ const char* psgpu_version(void);
 
 /* ---- device context ------------------------------------------------------ */
 int  psgpu_create(int deviceOrdinal, psgpu_ctx** out);
+/* Frees the context; waits for an in-flight compile of its model's kernels first (call
+ * it before the process exits: a compile must not run while the process tears down). */
 void psgpu_destroy(psgpu_ctx* ctx);
 int  psgpu_device_count(void);
 /* Upload a model (validates the op tree; builds the device walk program). */

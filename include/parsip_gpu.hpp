@@ -22,8 +22,10 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <type_traits>
+#include <vector>
 
 #include "parsip_gpu.h"
 
@@ -132,6 +134,329 @@ private:
     Context ctx_;
 };
 
+/* ---- BlobTree -> SoA linearizer + SimdPoly-shaped driver ---------------------------
+ * SimdPoly (Parsip100/ParsipHaptics/include/PS_HighPerformanceRender.h:15-33, bodies
+ * .cpp:42-426) on the device.  `Api` names the caller's BlobTree classes (the
+ * ParsipHaptics library: see parsip_gpu_blobtree.hpp; tests: a mock with the same methods):
+ *   Api::Node               CBlobNode: isOperator(), getNodeType() (_constSettings.h
+ *                           codes), countChildren(), getChild(i), getOctree().lower/.upper,
+ *                           getMaterial().diffused, getTransform().getBackwardMatrix()
+ *                           (isIdentity(), getRow(float*, int))
+ *   Api::SkeletonPrimitive  getSkeleton(); Api::SkeletonPoint/Line/Ring/Disc/Cylinder/Cube/
+ *                           Triangle with the reference getters
+ *   Api::Pcm, RicciBlend, WarpTwist, WarpTaper, WarpBend, WarpShear  operator parameters
+ * linearizeBlobTree follows the reference walk exactly: pre-order ids (an operator takes
+ * its id before its children; root op 0), opChildKind = isOpLeft * 2 + isOpRight, boxes
+ * from getOctree(), a non-identity backward matrix into the next 12-float row slot
+ * (rows 0-2), identity -> idxMatrix 0, Ricci resY = 1/n, -1/-2/-3 on prim / op overflow
+ * or a non-binary operator.  Two documented differences: node types are translated to
+ * the PS_Polygonizer.h enum the hot path switches on (translateTypes = false writes the
+ * raw BlobTree codes as the reference does, SURVEY.md §8(b) "Enum"), and a child's error
+ * code is returned instead of being stored as a child id; triangleCompat = true keeps the
+ * reference's Triangle packing bug (p2.z written into resX, .cpp:342-344). */
+namespace bt {  // _constSettings.h:26-38 (the caller-side BlobTree codes)
+enum : int {
+    PrimPoint = 0, PrimLine = 1, PrimCylinder = 2, PrimDisc = 3, PrimRing = 4, PrimPolygon = 5, PrimCube = 6,
+    PrimTriangle = 7, PrimNull = 12, OpUnion = 14, OpRicciBlend = 19, OpPcm = 22, OpWarpTwist = 24,
+    OpWarpTaper = 25, OpWarpBend = 26, OpWarpShear = 27
+};
+}  // namespace bt
+
+template <class Api>
+class SimdPolyT {
+public:
+    using Node = typename Api::Node;
+    static constexpr int kErrPrimOverflow = -1;      // PS_ERROR_PRIM_OVERFLOW (.cpp:10)
+    static constexpr int kErrOperatorOverflow = -2;  // PS_ERROR_OPERATOR_OVERFLOW
+    static constexpr int kErrNonBinaryOp = -3;       // PS_ERROR_NON_BINARY_OP
+
+    explicit SimdPolyT(int device = 0, bool translateTypes = true, bool triangleCompat = false)
+        : ctx_(device), translate_(translateTypes), triangleCompat_(triangleCompat) {
+        reset();
+    }
+
+    /* SimdPoly::reset (.cpp:31-38): empty SoA (zero-filled, so repeated linearizations
+     * give identical bytes). */
+    void reset() {
+        std::memset(&prims_, 0, sizeof(prims_));
+        std::memset(&ops_, 0, sizeof(ops_));
+        std::memset(&primMats_, 0, sizeof(primMats_));
+        std::memset(&boxMats_, 0, sizeof(boxMats_));
+        info_ = PsMeshInfo{};
+        haveMesh_ = false;
+    }
+
+    /* SimdPoly::linearizeBlobTree (.cpp:366-371): the root's id (0) or -1/-2/-3. */
+    int linearizeBlobTree(Node* root) {
+        reset();
+        int isOperator = 0;
+        return linearize(root, -1, isOperator);
+    }
+
+    /* SimdPoly::run (.cpp:373-376): upload the SoA and polygonize on the device (blocking;
+     * the compact mesh stays in HBM until draw / exportPolyMPUs / mesh). */
+    int run(float cellsize) {
+        if (!ctx_.ok()) return ctx_.status();
+        if (prims_.ctPrims == 0) return PSGPU_RET_PARAM_ERROR;  // Polygonize :322-323
+        int rc = psgpu_set_model(ctx_.get(), &prims_, &primMats_, &ops_);
+        if (rc == PSGPU_RET_SUCCESS) rc = psgpu_polygonize(ctx_.get(), cellsize, 0, 0xffffffffu, nullptr);
+        if (rc == PSGPU_RET_SUCCESS) rc = psgpu_finish(ctx_.get(), &info_);
+        haveMesh_ = false;
+        return rc;
+    }
+
+    /* SimdPoly::draw (.cpp:378-426) without GL: visits every MPU with triangles, in
+     * PolyMPUs order, as the arrays draw() hands to glColorPointer / glNormalPointer /
+     * glVertexPointer / glDrawElements: f(pos, nrm, col, ctVertices, tris (MPU-local
+     * U16 ids), ctTriangles). */
+    template <class F>
+    int draw(F&& perMpu) {
+        int rc = download();
+        if (rc != PSGPU_RET_SUCCESS) return rc;
+        std::vector<uint16_t> local;
+        for (uint32_t m = 0; m < info_.ctMPUs; ++m) {
+            const uint32_t v0 = (uint32_t)offs_[m], v1 = (uint32_t)offs_[m + 1];
+            const uint32_t t0 = (uint32_t)(offs_[m] >> 32), t1 = (uint32_t)(offs_[m + 1] >> 32);
+            if (t1 == t0) continue;
+            local.resize((size_t)(t1 - t0) * 3);
+            for (size_t i = 0; i < local.size(); ++i) local[i] = (uint16_t)(tris_[(size_t)t0 * 3 + i] - v0);
+            perMpu(&pos_[(size_t)v0 * 3], &nrm_[(size_t)v0 * 3], &col_[(size_t)v0 * 3], v1 - v0, local.data(), t1 - t0);
+        }
+        return PSGPU_RET_SUCCESS;
+    }
+
+    /* The PolyMPUs layout (vMPUs[0..ctMPUs)), for callers that keep the reference's arrays. */
+    template <class PolyMPUsT>
+    int exportPolyMPUs(PolyMPUsT& polyMPUs) {
+        static_assert(sizeof(polyMPUs.vMPUs[0]) == sizeof(PsMPU), "MPU layout");
+        const uint32_t capacity = (uint32_t)(sizeof(polyMPUs.vMPUs) / sizeof(polyMPUs.vMPUs[0]));
+        uint32_t ct = 0;
+        const int rc = psgpu_export_polympus(ctx_.get(), reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct);
+        polyMPUs.ctMPUs = rc == PSGPU_RET_SUCCESS ? ct : 0u;
+        return rc;
+    }
+
+    int mesh(PsMeshDevice* out) { return psgpu_mesh_device(ctx_.get(), out); }
+    const PsMeshInfo& info() const { return info_; }
+    const PsSoaBlobPrims& prims() const { return prims_; }
+    const PsSoaBlobOps& ops() const { return ops_; }
+    const PsSoaPrimMatrices& primMatrices() const { return primMats_; }
+    const PsSoaBoxMatrices& boxMatrices() const { return boxMats_; }
+    Context& context() { return ctx_; }
+
+private:
+    template <class V>
+    static void put3(float* x, float* y, float* z, int i, const V& v) {
+        x[i] = v.x;
+        y[i] = v.y;
+        z[i] = v.z;
+    }
+    uint8_t code(int blobTreeType) const {
+        if (!translate_) return (uint8_t)blobTreeType;
+        const int t = psgpu_translate_blobtree_type(blobTreeType);
+        return (uint8_t)(t < 0 ? blobTreeType : t);
+    }
+
+    int linearize(Node* root, int parentID, int& outIsOperator) {
+        if (parentID == -1) {  // .cpp:45-64: scene box from the root's octree, identity matrix slot 0
+            prims_.bboxLo = PsVec3f{root->getOctree().lower.x, root->getOctree().lower.y, root->getOctree().lower.z};
+            prims_.bboxHi = PsVec3f{root->getOctree().upper.x, root->getOctree().upper.y, root->getOctree().upper.z};
+            const float identity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+            primMats_.count = 1;
+            boxMats_.count = 1;
+            for (int i = 0; i < PSGPU_PRIM_MATRIX_STRIDE; ++i) primMats_.matrix[i] = identity[i];
+            for (int i = 0; i < PSGPU_BOX_MATRIX_STRIDE; ++i) boxMats_.matrix[i] = identity[i];
+        }
+        outIsOperator = root->isOperator() ? 1 : 0;
+        const int type = (int)root->getNodeType();
+        if (outIsOperator) {  // .cpp:67-161
+            if (ops_.ctOps >= PSGPU_MAX_TREE_NODES) return kErrOperatorOverflow;
+            const int cur = (int)ops_.ctOps++;
+            ops_.opType[cur] = code(type);
+            if (root->countChildren() != 2) return kErrNonBinaryOp;
+            int isOp[2] = {0, 0}, kid[2] = {0, 0};
+            for (int c = 0; c < 2; ++c) {
+                kid[c] = linearize(root->getChild(c), cur, isOp[c]);
+                if (kid[c] < 0) return kid[c];
+            }
+            ops_.opLeftChild[cur] = (uint8_t)kid[0];
+            ops_.opRightChild[cur] = (uint8_t)kid[1];
+            ops_.opChildKind[cur] = (uint8_t)(isOp[0] * 2 + isOp[1]);
+            put3(ops_.vBoxLoX, ops_.vBoxLoY, ops_.vBoxLoZ, cur, root->getOctree().lower);
+            put3(ops_.vBoxHiX, ops_.vBoxHiY, ops_.vBoxHiZ, cur, root->getOctree().upper);
+            switch (type) {
+            case bt::OpPcm: {
+                auto* n = reinterpret_cast<typename Api::Pcm*>(root);
+                ops_.resX[cur] = n->getPropagateLeft();
+                ops_.resY[cur] = n->getPropagateRight();
+                ops_.resZ[cur] = n->getAlphaLeft();
+                ops_.resW[cur] = n->getAlphaRight();
+            } break;
+            case bt::OpRicciBlend: {
+                const float nn = reinterpret_cast<typename Api::RicciBlend*>(root)->getN();
+                ops_.resX[cur] = nn;
+                if (nn != 0.0f) ops_.resY[cur] = 1.0f / nn;
+            } break;
+            case bt::OpWarpTwist: {
+                auto* n = reinterpret_cast<typename Api::WarpTwist*>(root);
+                ops_.resX[cur] = n->getWarpFactor();
+                ops_.resY[cur] = static_cast<float>(n->getMajorAxis());
+            } break;
+            case bt::OpWarpTaper: {
+                auto* n = reinterpret_cast<typename Api::WarpTaper*>(root);
+                ops_.resX[cur] = n->getWarpFactor();
+                ops_.resY[cur] = static_cast<float>(n->getAxisAlong());
+                ops_.resZ[cur] = static_cast<float>(n->getAxisTaper());
+            } break;
+            case bt::OpWarpBend: {
+                auto* n = reinterpret_cast<typename Api::WarpBend*>(root);
+                ops_.resX[cur] = n->getBendRate();
+                ops_.resY[cur] = n->getBendCenter();
+                ops_.resZ[cur] = n->getBendRegion().left;
+                ops_.resW[cur] = n->getBendRegion().right;
+            } break;
+            case bt::OpWarpShear: {
+                auto* n = reinterpret_cast<typename Api::WarpShear*>(root);
+                ops_.resX[cur] = n->getWarpFactor();
+                ops_.resY[cur] = static_cast<float>(n->getAxisAlong());
+                ops_.resZ[cur] = static_cast<float>(n->getAxisDependent());
+            } break;
+            default: break;
+            }
+            return cur;
+        }
+        // primitive (.cpp:162-363)
+        if (prims_.ctPrims >= PSGPU_MAX_TREE_NODES) return kErrPrimOverflow;
+        const int cur = (int)prims_.ctPrims++;
+        const auto d = root->getMaterial().diffused;
+        prims_.colorX[cur] = d.x;
+        prims_.colorY[cur] = d.y;
+        prims_.colorZ[cur] = d.z;
+        put3(prims_.vPrimBoxLoX, prims_.vPrimBoxLoY, prims_.vPrimBoxLoZ, cur, root->getOctree().lower);
+        put3(prims_.vPrimBoxHiX, prims_.vPrimBoxHiY, prims_.vPrimBoxHiZ, cur, root->getOctree().upper);
+        const auto back = root->getTransform().getBackwardMatrix();
+        if (back.isIdentity()) {
+            prims_.idxMatrix[cur] = 0;
+        } else {
+            const uint32_t k = primMats_.count;
+            prims_.idxMatrix[cur] = (uint8_t)k;
+            float row[16];
+            for (int r = 0; r < 4; ++r) back.getRow(&row[4 * r], r);
+            for (int i = 0; i < PSGPU_PRIM_MATRIX_STRIDE; ++i) primMats_.matrix[k * PSGPU_PRIM_MATRIX_STRIDE + i] = row[i];
+            primMats_.count++;
+        }
+        prims_.skeletType[cur] = code(type);
+        auto* sp = reinterpret_cast<typename Api::SkeletonPrimitive*>(root);
+        switch (type) {
+        case bt::PrimPoint: {
+            auto* s = reinterpret_cast<typename Api::SkeletonPoint*>(sp->getSkeleton());
+            put3(prims_.posX, prims_.posY, prims_.posZ, cur, s->getPosition());
+        } break;
+        case bt::PrimLine: {
+            auto* s = reinterpret_cast<typename Api::SkeletonLine*>(sp->getSkeleton());
+            put3(prims_.posX, prims_.posY, prims_.posZ, cur, s->getStartPosition());
+            put3(prims_.dirX, prims_.dirY, prims_.dirZ, cur, s->getEndPosition());
+        } break;
+        case bt::PrimRing:
+        case bt::PrimDisc: {
+            float r;
+            if (type == bt::PrimRing) {
+                auto* s = reinterpret_cast<typename Api::SkeletonRing*>(sp->getSkeleton());
+                put3(prims_.posX, prims_.posY, prims_.posZ, cur, s->getPosition());
+                put3(prims_.dirX, prims_.dirY, prims_.dirZ, cur, s->getDirection());
+                r = s->getRadius();
+            } else {
+                auto* s = reinterpret_cast<typename Api::SkeletonDisc*>(sp->getSkeleton());
+                put3(prims_.posX, prims_.posY, prims_.posZ, cur, s->getPosition());
+                put3(prims_.dirX, prims_.dirY, prims_.dirZ, cur, s->getDirection());
+                r = s->getRadius();
+            }
+            prims_.resX[cur] = r;
+            prims_.resY[cur] = r * r;
+        } break;
+        case bt::PrimCylinder: {
+            auto* s = reinterpret_cast<typename Api::SkeletonCylinder*>(sp->getSkeleton());
+            put3(prims_.posX, prims_.posY, prims_.posZ, cur, s->getPosition());
+            put3(prims_.dirX, prims_.dirY, prims_.dirZ, cur, s->getDirection());
+            prims_.resX[cur] = s->getRadius();
+            prims_.resY[cur] = s->getHeight();
+        } break;
+        case bt::PrimCube: {
+            auto* s = reinterpret_cast<typename Api::SkeletonCube*>(sp->getSkeleton());
+            put3(prims_.posX, prims_.posY, prims_.posZ, cur, s->getPosition());
+            prims_.resX[cur] = s->getSide();
+        } break;
+        case bt::PrimTriangle: {
+            auto* s = reinterpret_cast<typename Api::SkeletonTriangle*>(sp->getSkeleton());
+            const auto p0 = s->getTriangleCorner(0), p1 = s->getTriangleCorner(1), p2 = s->getTriangleCorner(2);
+            put3(prims_.posX, prims_.posY, prims_.posZ, cur, p0);
+            put3(prims_.dirX, prims_.dirY, prims_.dirZ, cur, p1);
+            prims_.resX[cur] = p2.x;
+            prims_.resY[cur] = p2.y;
+            if (triangleCompat_) prims_.resX[cur] = p2.z;  // the reference adapter's bug
+            else prims_.resZ[cur] = p2.z;
+        } break;
+        case bt::PrimNull:
+            prims_.posX[cur] = prims_.posY[cur] = prims_.posZ[cur] = 0.0f;
+            break;
+        default:  // "has not been implemented in compact mode yet" (.cpp:353-359): parameters stay 0
+            break;
+        }
+        return cur;
+    }
+
+    int download() {
+        if (haveMesh_) return PSGPU_RET_SUCCESS;
+        PsMeshInfo I;
+        int rc = psgpu_finish(ctx_.get(), &I);
+        if (rc != PSGPU_RET_SUCCESS) return rc;
+        info_ = I;
+        pos_.resize((size_t)I.ctVertices * 3);
+        nrm_.resize(pos_.size());
+        col_.resize(pos_.size());
+        tris_.resize((size_t)I.ctTriangles * 3);
+        offs_.resize((size_t)I.ctMPUs + 1);
+        rc = psgpu_download_mesh(ctx_.get(), pos_.data(), nrm_.data(), col_.data(), tris_.data(), offs_.data());
+        haveMesh_ = rc == PSGPU_RET_SUCCESS;
+        return rc;
+    }
+
+    Context ctx_;
+    bool translate_, triangleCompat_;
+    PsSoaBlobPrims prims_;
+    PsSoaBlobOps ops_;
+    PsSoaPrimMatrices primMats_;
+    PsSoaBoxMatrices boxMats_;
+    PsMeshInfo info_{};
+    bool haveMesh_ = false;
+    std::vector<float> pos_, nrm_, col_;
+    std::vector<uint32_t> tris_;
+    std::vector<uint64_t> offs_;
+};
+
 }  // namespace psgpu
+
+/* The reference's own names for the drop-in: a host that includes this header instead
+ * of PS_SimdPoly/include/PS_Polygonizer.h keeps calling PS::SIMDPOLY::Polygonize etc.
+ * (PS_Polygonizer.h:384-393) on its PS::SIMDPOLY SoA types.  Define PSGPU_NO_PS_NAMES
+ * when both headers must coexist. */
+#ifndef PSGPU_NO_PS_NAMES
+namespace PS {
+namespace SIMDPOLY {
+typedef PsSoaBlobPrims SOABlobPrims;
+typedef PsSoaBlobOps SOABlobOps;
+typedef PsSoaPrimMatrices SOABlobPrimMatrices;
+typedef PsSoaBoxMatrices SOABlobBoxMatrices;
+typedef PsMPU MPU;
+struct PolyMPUs {  /* PS_Polygonizer.h:196-198 */
+    MPU vMPUs[PSGPU_MAX_MPU_COUNT];
+    uint32_t ctMPUs;
+};
+using psgpu::CountMPUNeeded;
+using psgpu::Polygonize;
+using psgpu::PrepareBBoxes;
+}  // namespace SIMDPOLY
+}  // namespace PS
+#endif
 
 #endif /* PARSIP_GPU_HPP */

@@ -1,0 +1,45 @@
+/*
+ * parsip_gpu_blobtree.hpp — SimdPoly for ParsipHaptics' own BlobTree classes.
+ *
+ * Drop-in for Parsip100/ParsipHaptics/include/PS_HighPerformanceRender.h: include it
+ * (after the BlobTree library, Parsip100/PS_BlobTree/include/BlobTreeLibraryAll.h)
+ * instead of that header, and the layer that owns a SimdPoly (CLayerManager.h:70,135)
+ * keeps calling
+ *
+ *     SimdPoly poly;
+ *     poly.linearizeBlobTree(root);   // PS_HighPerformanceRender.cpp:366-371
+ *     poly.run(cellsize);             // :373-376, now on the MI355X
+ *     poly.draw(visitor);             // :378-426, the per-MPU arrays handed to GL
+ *
+ * The node classes named here are the reference's (PS::BLOBTREE, PS_BlobTree/include/):
+ * CBlobNode (CBlobTree.h:29), CSkeletonPrimitive (CSkeletonPrimitive.h:24), the skeletons
+ * CSkeletonPoint/Line/Ring/Disc/Cylinder/Cube/Triangle, and the operators CPcm,
+ * CRicciBlend, CWarpTwist, CWarpTaper, CWarpBend, CWarpShear.
+ */
+#ifndef PARSIP_GPU_BLOBTREE_HPP
+#define PARSIP_GPU_BLOBTREE_HPP
+
+#include "parsip_gpu.hpp"
+
+struct ParsipBlobTreeApi {
+    typedef PS::BLOBTREE::CBlobNode Node;
+    typedef PS::BLOBTREE::CSkeletonPrimitive SkeletonPrimitive;
+    typedef PS::BLOBTREE::CSkeletonPoint SkeletonPoint;
+    typedef PS::BLOBTREE::CSkeletonLine SkeletonLine;
+    typedef PS::BLOBTREE::CSkeletonRing SkeletonRing;
+    typedef PS::BLOBTREE::CSkeletonDisc SkeletonDisc;
+    typedef PS::BLOBTREE::CSkeletonCylinder SkeletonCylinder;
+    typedef PS::BLOBTREE::CSkeletonCube SkeletonCube;
+    typedef PS::BLOBTREE::CSkeletonTriangle SkeletonTriangle;
+    typedef PS::BLOBTREE::CPcm Pcm;
+    typedef PS::BLOBTREE::CRicciBlend RicciBlend;
+    typedef PS::BLOBTREE::CWarpTwist WarpTwist;
+    typedef PS::BLOBTREE::CWarpTaper WarpTaper;
+    typedef PS::BLOBTREE::CWarpBend WarpBend;
+    typedef PS::BLOBTREE::CWarpShear WarpShear;
+};
+
+/* class SimdPoly (PS_HighPerformanceRender.h:15-33) on the device. */
+typedef psgpu::SimdPolyT<ParsipBlobTreeApi> SimdPoly;
+
+#endif /* PARSIP_GPU_BLOBTREE_HPP */

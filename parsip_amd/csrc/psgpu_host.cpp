@@ -830,6 +830,8 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (cullEnv) c->cull = atoi(cullEnv) != 0;
     const char* jitEnv = getenv("PSGPU_JIT");
     if (jitEnv) c->useJit = std::min(2, std::max(0, atoi(jitEnv)));
+    const char* asyncEnv = getenv("PSGPU_JIT_ASYNC");
+    if (asyncEnv) c->jitAsync = atoi(asyncEnv) != 0;
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -839,6 +841,10 @@ void psgpu_destroy(psgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graphs(c);
+    // an in-flight hiprtc compile must not outlive its owner: a process that exits while
+    // LLVM compiles on the job thread tears LLVM's statics down under it
+    if (c->jitPending && c->jitFut.valid()) c->jitFut.wait();
+    c->jitFut = JitFuture();
     c->jit.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps};

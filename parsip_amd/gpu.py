@@ -14,8 +14,10 @@ There is no CPU fallback: if the HIP library or a GPU is missing, the calls rais
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -23,6 +25,8 @@ import numpy as np
 from . import soa
 
 _LIB = None
+_LIVE = weakref.WeakSet()  # contexts / groups closed at interpreter exit (psgpu_destroy
+                           # waits for an in-flight hiprtc compile: none may outlive the process)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libparsip_gpu.so")
 
 
@@ -229,6 +233,7 @@ class Polygonizer:
         self._L = L
         self.model = None
         self.info = None
+        _LIVE.add(self)
 
     def close(self):
         if getattr(self, "_ctx", None) and self._ctx.value:
@@ -405,6 +410,7 @@ class Group:
         _check(L.psgpu_group_create(devs, len(devices), ctypes.byref(self._g)), "psgpu_group_create")
         self._L = L
         self.n = len(devices)
+        _LIVE.add(self)
 
     def close(self):
         if getattr(self, "_g", None) and self._g.value:
@@ -509,3 +515,12 @@ class Comm:
         parts = (PsGroupPart * self.nranks)()
         _check(self._L.psgpu_comm_result(self._c, ctypes.byref(info), parts), "psgpu_comm_result")
         return info, list(parts)
+
+
+@atexit.register
+def _close_live():
+    for obj in list(_LIVE):
+        try:
+            obj.close()
+        except Exception:  # noqa: BLE001 (best effort at exit)
+            pass

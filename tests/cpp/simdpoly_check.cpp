@@ -1,0 +1,155 @@
+// The C++ drop-in faces compiled as a ParsipHaptics host would use them:
+//
+//   tree <tree.txt> <soa.bin> [translate compat]
+//        SimdPoly (include/parsip_gpu_blobtree.hpp) over the mock BlobTree: linearizeBlobTree
+//        of the pre-order tree file written by tests/test_cpp_simdpoly.py; writes the return
+//        code and the SoA bytes (prims | prim matrices | ops | box matrices).
+//   run <tree.txt> <cellsize> <mesh.bin>
+//        the same, then SimdPoly::run on device 0 and SimdPoly::draw's per-MPU arrays
+//        (ctV, ctT, pos, nrm, col, U16 triangles per drawn MPU) into mesh.bin.
+//   soa <soa.bin> <cellsize> <polympus.bin>
+//        PS::SIMDPOLY::Polygonize on a PS::SIMDPOLY::PolyMPUs (24,000 MPUs, the reference's
+//        capacity); writes rc, ctMPUs and the MPUs.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "mock_blobtree.hpp"
+#include "parsip_gpu_blobtree.hpp"
+
+using namespace PS::BLOBTREE;
+
+namespace {
+
+// One node per line, pre-order: type nKids lo3 hi3 diffuse3 identity back16 params12
+// (params: a3 b3 c3 r h and res0..3 for operators, as the writer documents).
+CBlobNode* read_node(std::istream& in, std::vector<std::unique_ptr<CBlobNode>>& own) {
+    int type, nk;
+    in >> type >> nk;
+    if (!in) return nullptr;
+    float v[3 + 3 + 3 + 1 + 16 + 12];
+    for (float& f : v) in >> f;
+    CBlobNode* n;
+    if (type >= 14) {
+        switch (type) {
+        case 19: n = new CRicciBlend(); break;
+        case 22: n = new CPcm(); break;
+        case 24: n = new CWarpTwist(); break;
+        case 25: n = new CWarpTaper(); break;
+        case 26: n = new CWarpBend(); break;
+        case 27: n = new CWarpShear(); break;
+        default: n = new CBlobNode(); break;
+        }
+    } else {
+        CSkeletonPrimitive* sp = new CSkeletonPrimitive();
+        CSkeleton* s;
+        switch (type) {
+        case 0: s = new CSkeletonPoint(); break;
+        case 1: s = new CSkeletonLine(); break;
+        case 2: s = new CSkeletonCylinder(); break;
+        case 3: s = new CSkeletonDisc(); break;
+        case 4: s = new CSkeletonRing(); break;
+        case 6: s = new CSkeletonCube(); break;
+        case 7: s = new CSkeletonTriangle(); break;
+        default: s = new CSkeleton(); break;
+        }
+        const float* q = v + 26;
+        s->a = vec3f{q[0], q[1], q[2]};
+        s->b = vec3f{q[3], q[4], q[5]};
+        s->c = vec3f{q[6], q[7], q[8]};
+        s->r = q[9];
+        s->h = q[10];
+        sp->skeleton = s;
+        n = sp;
+    }
+    own.emplace_back(n);
+    n->type = type;
+    n->octree.lower = vec3f{v[0], v[1], v[2]};
+    n->octree.upper = vec3f{v[3], v[4], v[5]};
+    n->material.diffused = vec4f{v[6], v[7], v[8], 1.0f};
+    n->transform.back.identity = v[9] != 0.0f;
+    std::memcpy(n->transform.back.e, v + 10, 64);
+    for (int k = 0; k < 4; ++k) n->res[k] = v[26 + k];
+    for (int c = 0; c < nk; ++c) n->kids.push_back(read_node(in, own));
+    return n;
+}
+
+template <class T>
+void put(std::ofstream& o, const T& x) { o.write(reinterpret_cast<const char*>(&x), sizeof(T)); }
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 4) return 64;
+    const std::string mode = argv[1];
+    if (mode == "tree" || mode == "run") {
+        std::ifstream in(argv[2]);
+        std::vector<std::unique_ptr<CBlobNode>> own;
+        CBlobNode* root = read_node(in, own);
+        if (!root) return 65;
+        const bool translate = argc > 4 && mode == "tree" ? std::atoi(argv[4]) != 0 : true;
+        const bool compat = argc > 5 && mode == "tree" ? std::atoi(argv[5]) != 0 : false;
+        std::unique_ptr<SimdPoly> poly(new SimdPoly(0, translate, compat));
+        const int code = poly->linearizeBlobTree(root);
+        if (mode == "tree") {
+            std::ofstream o(argv[3], std::ios::binary);
+            put(o, code);
+            put(o, poly->prims());
+            put(o, poly->primMatrices());
+            put(o, poly->ops());
+            put(o, poly->boxMatrices());
+            return 0;
+        }
+        if (code < 0) return 66;
+        const float cs = (float)std::atof(argv[3]);
+        std::fprintf(stderr, "linearized %d prims\n", (int)poly->prims().ctPrims);
+        const int rc = poly->run(cs);
+        std::fprintf(stderr, "ran %d\n", rc);
+        std::printf("run rc %d V %u T %u\n", rc, poly->info().ctVertices, poly->info().ctTriangles);
+        if (rc != PSGPU_RET_SUCCESS) return 67;
+        std::ofstream o(argv[4], std::ios::binary);
+        uint32_t drawn = 0;
+        const int dr = poly->draw([&](const float* pos, const float* nrm, const float* col, uint32_t nv,
+                                      const uint16_t* tris, uint32_t nt) {
+            put(o, nv);
+            put(o, nt);
+            o.write(reinterpret_cast<const char*>(pos), (std::streamsize)nv * 12);
+            o.write(reinterpret_cast<const char*>(nrm), (std::streamsize)nv * 12);
+            o.write(reinterpret_cast<const char*>(col), (std::streamsize)nv * 12);
+            o.write(reinterpret_cast<const char*>(tris), (std::streamsize)nt * 6);
+            ++drawn;
+        });
+        std::fprintf(stderr, "drawn %u\n", drawn);
+        o.close();
+        poly.reset();
+        std::fprintf(stderr, "destroyed\n");
+        return dr == PSGPU_RET_SUCCESS ? 0 : 68;
+    }
+    if (mode == "soa" && argc >= 5) {
+        static PS::SIMDPOLY::SOABlobPrims prims;
+        static PS::SIMDPOLY::SOABlobPrimMatrices mats;
+        static PS::SIMDPOLY::SOABlobOps ops;
+        static PS::SIMDPOLY::SOABlobBoxMatrices boxes;
+        std::ifstream in(argv[2], std::ios::binary);
+        in.read(reinterpret_cast<char*>(&prims), sizeof prims);
+        in.read(reinterpret_cast<char*>(&mats), sizeof mats);
+        in.read(reinterpret_cast<char*>(&ops), sizeof ops);
+        in.read(reinterpret_cast<char*>(&boxes), sizeof boxes);
+        if (!in) return 65;
+        std::unique_ptr<PS::SIMDPOLY::PolyMPUs> poly(new PS::SIMDPOLY::PolyMPUs());
+        poly->ctMPUs = 12345;  // must be overwritten (0 on failure)
+        const int rc = PS::SIMDPOLY::Polygonize((float)std::atof(argv[3]), prims, mats, ops, *poly);
+        std::printf("Polygonize rc %d ctMPUs %u\n", rc, poly->ctMPUs);
+        std::ofstream o(argv[4], std::ios::binary);
+        put(o, rc);
+        put(o, poly->ctMPUs);
+        o.write(reinterpret_cast<const char*>(poly->vMPUs), (std::streamsize)poly->ctMPUs * sizeof(PsMPU));
+        return 0;
+    }
+    return 64;
+}

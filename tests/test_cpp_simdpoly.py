@@ -1,0 +1,212 @@
+"""The C++ drop-in faces (include/parsip_gpu.hpp, include/parsip_gpu_blobtree.hpp) compiled
+as a host would compile them, against a mock of the ParsipHaptics BlobTree classes
+(tests/cpp/mock_blobtree.hpp: the accessors SimdPoly::linearizeBlobTree calls,
+PS_HighPerformanceRender.cpp:42-364).
+
+CPU: the C++ linearizer gives the same SoA bytes as the Python mirror
+(parsip_amd/blobtree.py) on the reference's own train scene and on a tree with every
+primitive and parametrised operator, in translated and raw-code modes.
+GPU: SimdPoly::run + draw on the device against the oracle, and
+PS::SIMDPOLY::Polygonize into the reference-capacity PolyMPUs (C2 fits; C3 returns -4
+with ctMPUs = 0)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from parsip_amd import blobtree as bt
+from parsip_amd import gpu, soa, synth
+from parsip_amd.blobtree import BlobNodeType as B
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="module")
+def exe(tmp_path_factory):
+    gpp = shutil.which("g++")
+    if gpp is None:
+        pytest.skip("no g++")
+    gpu.load()
+    out = tmp_path_factory.mktemp("cpp") / "simdpoly_check"
+    lib_dir = os.path.join(ROOT, "parsip_amd")
+    subprocess.run([gpp, "-std=c++17", "-O1", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "tests", "cpp"), os.path.join(ROOT, "tests", "cpp", "simdpoly_check.cpp"),
+                    "-L", lib_dir, "-l:libparsip_gpu.so", f"-Wl,-rpath,{lib_dir}", "-o", str(out)], check=True)
+    return str(out)
+
+
+def _v3(x):
+    return [float(np.float32(c)) for c in x]
+
+
+def write_tree(root: bt.BlobNode, path: str) -> None:
+    """Pre-order node records for the mock (see simdpoly_check.cpp read_node)."""
+    if root.octree is None:
+        bt.compute_octrees(root)
+    lines = []
+
+    def rec(n):
+        if n.octree is None:
+            bt.compute_octrees(n)
+        lo, hi = n.octree
+        back = n.transform.backward()
+        rows = np.concatenate([back.row(r) for r in range(4)])
+        p = n.params
+        q = [0.0] * 12
+        t = n.node_type
+        if n.is_operator():
+            if t == B.OP_RICCIBLEND:
+                q[0] = p.get("n", 2.0)
+            elif t == B.OP_PCM:
+                q[:4] = [p.get(k, 0.0) for k in ("propagate_left", "propagate_right", "alpha_left", "alpha_right")]
+            else:
+                q[:4] = [p.get(f"res{k}", 0.0) for k in "XYZW"]
+        elif t == B.PRIM_POINT:
+            q[0:3] = p["position"]
+        elif t == B.PRIM_LINE:
+            q[0:3], q[3:6] = p["start"], p["end"]
+        elif t in (B.PRIM_CYLINDER, B.PRIM_DISC, B.PRIM_RING):
+            q[0:3], q[3:6], q[9] = p["position"], p["direction"], p["radius"]
+            q[10] = p.get("height", 0.0)
+        elif t == B.PRIM_CUBE:
+            q[0:3], q[9] = p["position"], p["side"]
+        elif t == B.PRIM_TRIANGLE:
+            q[0:3], q[3:6], q[6:9] = p["corners"]
+        vals = [*_v3(lo), *_v3(hi), *_v3(n.material.diffused[:3]), 1.0 if back.is_identity() else 0.0,
+                *[float(x) for x in rows], *[float(np.float32(x)) for x in q]]
+        lines.append(f"{int(t)} {len(n.children)} " + " ".join(repr(v) for v in vals))
+        for c in n.children:
+            rec(c)
+
+    rec(root)
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def cpp_linearize(exe, root, tmp_path, translate=True, compat=False):
+    tree, out = tmp_path / "tree.txt", tmp_path / "soa.bin"
+    write_tree(root, str(tree))
+    subprocess.run([exe, "tree", str(tree), str(out), str(int(translate)), str(int(compat))], check=True, timeout=60)
+    raw = open(out, "rb").read()
+    code = int(np.frombuffer(raw[:4], np.int32)[0])
+    return code, raw[4:]
+
+
+def py_bytes(model: soa.Model) -> bytes:
+    return model.prims.tobytes() + model.mats.tobytes() + model.ops.tobytes() + model.boxmats.tobytes()
+
+
+def all_types_tree():
+    """Every primitive the adapter packs, every parametrised operator, matrices."""
+    aff = bt.Affine(scale=(1.2, 0.8, 1.0), rotate=(0.0, 0.38268343, 0.0, 0.9238795), translate=(0.3, -0.2, 0.1))
+    prims = [bt.Point((0.1, 0.2, 0.3)), bt.Line((-0.5, 0.0, 0.0), (0.5, 0.1, 0.0), transform=aff),
+             bt.Cylinder((0.0, -0.3, 0.0), (0.0, 1.0, 0.0), 0.2, 0.6), bt.Disc((0.3, 0.3, 0.0), (0.0, 0.0, 1.0), 0.4),
+             bt.Ring((-0.3, 0.3, 0.0), (1.0, 0.0, 0.0), 0.35, transform=aff), bt.Cube((0.0, 0.0, 0.4), 0.25),
+             bt.Triangle((0.0, 0.0, 0.0), (0.5, 0.0, 0.1), (0.0, 0.5, 0.2)), bt.Null()]
+    a = bt.Op(B.OP_RICCIBLEND, prims[0], prims[1], n=4.0)
+    b = bt.Op(B.OP_PCM, prims[2], prims[3], propagate_left=0.5, propagate_right=0.25, alpha_left=2.0,
+              alpha_right=3.0)
+    c = bt.Op(B.OP_WARPBEND, bt.Op(B.OP_UNION, prims[4], prims[5]), prims[6], resX=0.7, resY=0.1, resZ=-1.0,
+              resW=1.0)
+    d = bt.Op(B.OP_WARPTWIST, prims[7], bt.Point((0.9, 0.9, 0.9)), resX=0.3, resY=1.0)
+    e = bt.Op(B.OP_WARPSHEAR, bt.Op(B.OP_WARPTAPER, a, b, resX=0.2, resY=2.0, resZ=0.0), c, resX=0.1, resY=1.0,
+              resZ=2.0)
+    return bt.Op(B.OP_DIF, e, d)
+
+
+def train_tree():
+    from parsip_amd import scene
+
+    return bt.binarize(scene.load_scene(os.path.join(GOLDEN, "train_corrected.scene"))[0])
+
+
+@pytest.mark.parametrize("translate,compat", [(True, False), (False, True), (True, True)])
+def test_cpp_linearizer_all_types(exe, tmp_path, translate, compat):
+    root = all_types_tree()
+    code, raw = cpp_linearize(exe, root, tmp_path, translate, compat)
+    pcode, model = bt.linearize_blobtree(root, raw_types=not translate, triangle_compat=compat)
+    assert code == pcode == 0
+    assert raw == py_bytes(model)
+
+
+def test_cpp_linearizer_train_scene(exe, tmp_path):
+    root = train_tree()
+    code, raw = cpp_linearize(exe, root, tmp_path)
+    pcode, model = bt.linearize_blobtree(root)
+    assert code == pcode == 0 and model.ct_prims == 95
+    assert raw == py_bytes(model)
+
+
+def test_cpp_linearizer_errors(exe, tmp_path):
+    """-3 for a non-binary operator (PS_ERROR_NON_BINARY_OP), -1 past 128 primitives."""
+    tri = bt.Op(B.OP_UNION, bt.Point((0, 0, 0)), bt.Point((1, 0, 0)), bt.Point((0, 1, 0)))
+    assert cpp_linearize(exe, bt.Op(B.OP_BLEND, tri, bt.Point((0, 0, 1))), tmp_path)[0] == -3
+    acc = bt.Point((0, 0, 0))
+    for i in range(129):
+        acc = bt.Op(B.OP_BLEND, acc, bt.Point((0.01 * i, 0, 0)))
+    code, _ = cpp_linearize(exe, acc, tmp_path)
+    assert code == bt.linearize_blobtree(acc)[0] in (-1, -2)
+
+
+@pytest.mark.gpu
+def test_cpp_simdpoly_run_and_draw_train(exe, tmp_path, oracle):
+    """SimdPoly::linearizeBlobTree + run + draw (compiled C++) on the device, against the
+    oracle on the same SoA: every drawn MPU's arrays bit-exact."""
+    from parity_util import assert_bits_equal
+
+    root = train_tree()
+    tree, mesh = tmp_path / "tree.txt", tmp_path / "mesh.bin"
+    write_tree(root, str(tree))
+    r = subprocess.run([exe, "run", str(tree), "0.2", str(mesh)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    _, model = bt.linearize_blobtree(root)
+    om = oracle.polygonize(model, 0.2, threads=8)
+    raw = open(mesh, "rb").read()
+    at, drawn = 0, 0
+    for i in np.flatnonzero(om.stats[:, 3]):  # draw() visits MPUs with triangles, in order
+        nv, nt = np.frombuffer(raw[at:at + 8], np.uint32)
+        at += 8
+        assert (nv, nt) == (om.stats[i, 2], om.stats[i, 3])
+        v0, t0 = om.vertex_offsets[i], om.triangle_offsets[i]
+        for arr, ref, what in (("pos", om.pos, "pos"), ("nrm", om.nrm, "nrm"), ("col", om.col, "col")):
+            got = np.frombuffer(raw[at:at + nv * 12], np.float32).reshape(-1, 3)
+            at += nv * 12
+            assert_bits_equal(got, ref[v0:v0 + nv], what)
+        tris = np.frombuffer(raw[at:at + nt * 6], np.uint16).reshape(-1, 3)
+        at += nt * 6
+        np.testing.assert_array_equal(tris, om.tris[t0:t0 + nt])
+        drawn += 1
+    assert at == len(raw) and drawn > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_cpp_ps_simdpoly_polygonize(exe, tmp_path, oracle, name):
+    """PS::SIMDPOLY::Polygonize (the reference's free function and PolyMPUs type, 24,000
+    MPUs) through the compiled shim: C2 fills it bit-exactly; C3 (50,653 MPUs) does not
+    fit and returns -4 with ctMPUs = 0 (the reference truncates silently)."""
+    model, cs, _ = synth.make_config(name)
+    src, out = tmp_path / "soa.bin", tmp_path / "mpus.bin"
+    with open(src, "wb") as f:
+        f.write(model.prims.tobytes() + model.mats.tobytes() + model.ops.tobytes() + model.boxmats.tobytes())
+    r = subprocess.run([exe, "soa", str(src), repr(float(cs)), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(out, "rb").read()
+    rc, ct = np.frombuffer(raw[:8], np.int32)
+    if name == "C3":
+        assert (rc, ct) == (soa.RET_MPU_OVERFLOW, 0)
+        return
+    assert rc == soa.RET_SUCCESS and ct == 6859
+    mpus = np.frombuffer(raw[8:], soa.MPU_DTYPE)
+    om = oracle.polygonize(model, cs, threads=8)
+    np.testing.assert_array_equal(mpus["ctVertices"], om.stats[:, 2])
+    np.testing.assert_array_equal(mpus["ctTriangles"], om.stats[:, 3])
+    for i in np.flatnonzero(om.stats[:, 2]):
+        nv, nt = om.stats[i, 2], om.stats[i, 3]
+        v0, t0 = om.vertex_offsets[i], om.triangle_offsets[i]
+        assert mpus["vPos"][i, :nv * 3].tobytes() == om.pos[v0:v0 + nv].tobytes()
+        np.testing.assert_array_equal(mpus["triangles"][i, :nt * 3].reshape(-1, 3), om.tris[t0:t0 + nt])
