@@ -22,10 +22,11 @@ SoA although the SIMD path switches on the PS_Polygonizer.h enum (SURVEY.md §0 
 reference's bytes).
 
 Matrices are restated in fp32 exactly as CMatrix does them (PS_Matrix.h:124-145,
-416-446, 548-604; CQuaternion::toMatrix PS_Quaternion.h:368-394).  Octree boxes are not
-restated from the BlobTree library: each node's box is the conservative world AABB of
-its skeleton's support (8 transformed corners), and an operator's box is the union of
-its children's.
+416-446, 548-604; CQuaternion::toMatrix PS_Quaternion.h:368-394).  Node boxes are the
+octrees ParsipHaptics computes after loading a model (CLayer::recursive_RecomputeAllOctrees,
+CLayerManager.cpp:629-646: skeleton bounds, two corners through the accumulated forward
+matrix, per-operator union / first child / intersection / warp growth), restated in fp32
+(``compute_octrees_reference``); ``octrees="aabb"`` uses conservative world AABBs instead.
 """
 from __future__ import annotations
 
@@ -306,10 +307,20 @@ def _local_support_box(n: BlobNode):
     return np.zeros(3) - iso, np.zeros(3) + iso
 
 
-def compute_octrees(n: BlobNode):
-    """Fill every node's octree box bottom-up (conservative world AABBs)."""
+def compute_octrees(n: BlobNode, method: str = "reference"):
+    """Fill every node's octree box: "reference" (default) as ParsipHaptics computes them
+    for SimdPoly (compute_octrees_reference), or "aabb", conservative world AABBs of each
+    skeleton's support (8 transformed corners; an operator's box is the union)."""
+    if method == "reference":
+        return compute_octrees_reference(n)
+    if method != "aabb":
+        raise ValueError(f"unknown octree method {method!r}")
+    return compute_octrees_aabb(n)
+
+
+def compute_octrees_aabb(n: BlobNode):
     if n.is_operator():
-        boxes = [compute_octrees(c) for c in n.children]
+        boxes = [compute_octrees_aabb(c) for c in n.children]
         lo = np.min([b[0] for b in boxes], axis=0)
         hi = np.max([b[1] for b in boxes], axis=0)
     else:
@@ -319,6 +330,83 @@ def compute_octrees(n: BlobNode):
                    for i in range(8)]
         lo = np.min(corners, axis=0).astype(np.float64)
         hi = np.max(corners, axis=0).astype(np.float64)
+    n.octree = (np.asarray(lo, np.float32), np.asarray(hi, np.float32))
+    return n.octree
+
+
+ISO_VALUE = _F(0.5)  # _constSettings.h:10
+OCTREE_EXPANSION = _F(0.6)  # BOUNDING_OCTREE_EXPANSION_FACTOR, _constSettings.h:4
+
+
+def _skeleton_bound(n: BlobNode):
+    """CSkeleton*::bound() in local coordinates, fp32 in the reference's operation order
+    (CSkeletonPoint.h:59-64, CSkeletonLine.h:80-85, CSkeletonCylinder.h:103-110,
+    CSkeletonDisc.h:93-100, CSkeletonRing.h:107-114, CSkeletonCube.h:175-182,
+    CSkeletonTriangle.h:326-333, CNullPrimitive.h:25-30).  BBOX keeps the corners as given
+    (PS_BoundingBox.h:17): a Line or Cylinder along a negative direction gives lo > hi."""
+    p = n.params
+    t = n.node_type
+    iso = ISO_VALUE
+    v = lambda x: np.asarray(x, np.float32)  # noqa: E731
+    if t == BlobNodeType.PRIM_POINT:
+        c = v(p["position"])
+        return c - iso, c + iso
+    if t == BlobNodeType.PRIM_LINE:
+        a, b = v(p["start"]), v(p["end"])
+        e = iso + (_F(3.0) * iso) * (b - a)
+        return a - e, b + e
+    if t == BlobNodeType.PRIM_CYLINDER:
+        s0, d = v(p["position"]), v(p["direction"])
+        s1 = s0 + _F(p["height"]) * d
+        e = (iso + _F(p["radius"])) * v((1.0, 1.0, 1.0)) + (_F(0.5) * iso) * d
+        return s0 - e, s1 + e
+    if t in (BlobNodeType.PRIM_DISC, BlobNodeType.PRIM_RING):
+        c, d = v(p["position"]), v(p["direction"])
+        r = _F(_F(p["radius"]) + iso)
+        e = r * (v((1.0, 1.0, 1.0)) - d) + iso * d
+        return c - e, c + e
+    if t == BlobNodeType.PRIM_CUBE:
+        c = v(p["position"])
+        ss = _F(_F(p["side"]) + iso)
+        return c - ss, c + ss
+    if t == BlobNodeType.PRIM_TRIANGLE:
+        cs = v(p["corners"])
+        return cs.min(axis=0) - iso, cs.max(axis=0) + iso
+    return v((0.0, 0.0, 0.0)), v((0.0, 0.0, 0.0))
+
+
+def compute_octrees_reference(n: BlobNode, branch: "Matrix | None" = None):
+    """The octrees ParsipHaptics hands SimdPoly after loading a model:
+    CLayer::recursive_RecomputeAllOctrees (CLayerManager.cpp:629-646).  A primitive's box
+    is its skeleton bound with only its two corners mapped by the accumulated forward
+    matrix (COctree::transform, PS_Octree.cpp:342-348); an operator's box is the union of
+    its children (Union, Blend, RicciBlend, GradientBlend, PCM), its first child
+    (Difference, SmoothDifference), their csgIntersection (Intersection) or its first
+    child grown by 0.6 (the warps) (the operators' computeOctree, PS_BlobTree/include)."""
+    cur = (branch.copy() if branch is not None else Matrix())
+    cur.multiply(n.transform.forward())
+    if n.is_operator():
+        boxes = [compute_octrees_reference(c, cur) for c in n.children]
+        t = n.node_type
+        lo, hi = boxes[0][0].copy(), boxes[0][1].copy()
+        if t in (BlobNodeType.OP_DIF, BlobNodeType.OP_SMOOTHDIF):
+            pass
+        elif t == BlobNodeType.OP_INTERSECT:
+            for blo, bhi in boxes[1:]:
+                for a in range(3):  # COctree::csgIntersection (PS_Octree.cpp:362-380)
+                    if lo[a] <= bhi[a] and hi[a] >= blo[a]:
+                        lo[a] = max(lo[a], blo[a])
+                        hi[a] = min(hi[a], bhi[a])
+        elif t in (BlobNodeType.OP_WARPTWIST, BlobNodeType.OP_WARPTAPER, BlobNodeType.OP_WARPBEND,
+                   BlobNodeType.OP_WARPSHEAR):
+            lo, hi = lo - OCTREE_EXPANSION, hi + OCTREE_EXPANSION
+        else:
+            for blo, bhi in boxes[1:]:
+                lo, hi = np.minimum(lo, blo), np.maximum(hi, bhi)
+    else:
+        blo, bhi = _skeleton_bound(n)
+        lt, ht = cur.transform(blo), cur.transform(bhi)
+        lo, hi = np.minimum(lt, ht), np.maximum(lt, ht)
     n.octree = (np.asarray(lo, np.float32), np.asarray(hi, np.float32))
     return n.octree
 
@@ -339,14 +427,21 @@ def _translate(code: int, raw: bool) -> int:
     return int(code) if raw else soa.translate_blobtree_type(int(code))
 
 
-def linearize_blobtree(root: BlobNode, raw_types: bool = False, triangle_compat: bool = False):
+def linearize_blobtree(root: BlobNode, raw_types: bool = False, triangle_compat: bool = False,
+                       octrees: str = "reference"):
     """SimdPoly::linearizeBlobTree (PS_HighPerformanceRender.cpp:42-371, 366-371).
 
+    Node boxes are the nodes' octrees (getOctree(), :47-50, 97-107, 176-187); nodes without
+    one get them from compute_octrees(root, octrees) first.
     Returns (code, Model): code is the root's id (0) or a negative PS_ERROR_* code."""
     model = soa.Model.empty("blobtree")
     P, O, PM, BM = model.prims, model.ops, model.mats, model.boxmats
-    if root.octree is None:
-        compute_octrees(root)
+
+    def missing(n):
+        return n.octree is None or any(missing(c) for c in n.children)
+
+    if missing(root):
+        compute_octrees(root, octrees)
     lo, hi = root.octree
     P["bboxLo"][0] = lo
     P["bboxHi"][0] = hi
@@ -356,8 +451,6 @@ def linearize_blobtree(root: BlobNode, raw_types: bool = False, triangle_compat:
     BM["count"][0] = 1
 
     def rec(n: BlobNode):
-        if n.octree is None:
-            compute_octrees(n)
         nlo, nhi = n.octree
         if n.is_operator():
             if int(O["ctOps"][0]) >= soa.MAX_TREE_NODES:

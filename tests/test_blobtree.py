@@ -160,3 +160,47 @@ def test_scene_parser_variants():
     assert root.children[1].params["end"] == (1.0, 1.0, 1.0)
     with pytest.raises(scene.SceneError):
         scene.load_scene("[BLOBNODE 0]\nIsOperator=0\nPrimitiveType=TEAPOT\n[Global]\nRootIDs=(0)\n", from_text=True)
+
+
+def test_reference_octrees_follow_the_app():
+    """compute_octrees_reference restates CLayer::recursive_RecomputeAllOctrees
+    (CLayerManager.cpp:629-646): skeleton bounds in local coordinates (ISO_VALUE 0.5),
+    only the two corners through the accumulated forward matrix, Difference keeps its
+    first child's box, warps grow it by 0.6, blends take the union."""
+    import numpy as np
+
+    from parsip_amd import blobtree as bt
+    from parsip_amd.blobtree import BlobNodeType as B
+
+    p = bt.Point((1.0, 2.0, 3.0))
+    q = bt.Point((0.0, 0.0, 0.0), transform=bt.Affine(translate=(5.0, 0.0, 0.0)))
+    line = bt.Line((0.0, 0.0, 0.0), (-1.0, 0.0, 0.0))  # BBOX keeps its corners: lo > hi on x
+    root = bt.Op(B.OP_DIF, bt.Op(B.OP_BLEND, p, q), bt.Op(B.OP_WARPTWIST, line, bt.Point((9.0, 9.0, 9.0))))
+    bt.compute_octrees_reference(root)
+    np.testing.assert_array_equal(p.octree[0], [0.5, 1.5, 2.5])
+    np.testing.assert_array_equal(q.octree[0], [4.5, -0.5, -0.5])
+    np.testing.assert_array_equal(root.children[0].octree[0], [0.5, -0.5, -0.5])
+    np.testing.assert_array_equal(root.children[0].octree[1], [5.5, 2.5, 3.5])
+    np.testing.assert_array_equal(root.octree[0], root.children[0].octree[0])  # Difference: first child
+    # Line bound: start - (0.5 + 1.5 * (end - start)), end + ... -> x: 1.0 .. -2.0, min/max after transform
+    np.testing.assert_array_equal(line.octree[0], np.float32([-2.0, -0.5, -0.5]))
+    np.testing.assert_array_equal(root.children[1].octree[0], line.octree[0] - np.float32(0.6))
+
+
+def test_train_scene_reference_lattice():
+    """The reference's own scene with the app's octrees: the SimdPoly lattice at the
+    ParsipHaptics_Release.ini cellsize (0.14, GRID_DIM 8) and the box the CSV run used."""
+    import os
+
+    import numpy as np
+
+    from parsip_amd import blobtree as bt
+    from parsip_amd import gpu, scene
+
+    root = scene.load_scene(os.path.join(os.path.dirname(__file__), "golden", "train_corrected.scene"))[0]
+    code, model = bt.linearize_blobtree(bt.binarize(root))
+    assert code == 0 and model.ct_prims == 95
+    lo, hi = model.bbox
+    np.testing.assert_allclose(lo, [-5.153809, -1.25, -4.2197604], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(hi, [19.996407, 11.377769, 4.18024], rtol=0, atol=1e-6)
+    assert gpu.count_mpus(np.float32(0.14), lo, hi) == 26 * 13 * 9

@@ -45,12 +45,10 @@ def _v3(x):
 def write_tree(root: bt.BlobNode, path: str) -> None:
     """Pre-order node records for the mock (see simdpoly_check.cpp read_node)."""
     if root.octree is None:
-        bt.compute_octrees(root)
+        bt.compute_octrees(root)  # the linearizer's default (reference octrees)
     lines = []
 
     def rec(n):
-        if n.octree is None:
-            bt.compute_octrees(n)
         lo, hi = n.octree
         back = n.transform.backward()
         rows = np.concatenate([back.row(r) for r in range(4)])
