@@ -299,21 +299,31 @@ def main():
         if not ok:
             sys.exit(f"bench.py rank {grp.rank}: parts {counts} do not add up to the full grid {check['full']}")
 
-    # roofline pass: per-kernel hipEvent timing on the library's stream, one context over
-    # the rank's whole range (single stream: per-launch figures comparable with rocprof)
-    poly.set_option(gpu.OPT_KERNEL_TIMING, 1)
-    kt = {}
+    # roofline pass: per-kernel hipEvent timing on the library's stream(s), the same engine and
+    # split as the timed steps (each part's kernels on its own stream), so the per-launch
+    # averages are those of a rocprofv3 kernel trace of this command
+    eng.set_option(gpu.OPT_KERNEL_TIMING, 1)
+    kt_sum, launches, fmpus = {}, 0, 0
     reps = max(3, min(args.steps, 20))
     for _ in range(reps):
-        poly.run(cs, begin, end)
-        for k, v in poly.kernel_times().items():
-            kt[k] = kt.get(k, 0.0) + v / reps
-    poly.set_option(gpu.OPT_KERNEL_TIMING, 0)
-    single = poly.finish()  # the counts of that single-stream run
+        if nstreams > 1:
+            _, parts = eng.run(cs)
+            per_part = [eng.kernel_times(i) for i in range(nstreams)]
+            fmpus += sum(pt.info.ctFieldMPUs for pt in parts)
+        else:
+            fmpus += poly.run(cs, begin, end).ctFieldMPUs
+            per_part = [poly.kernel_times()]
+        for t in per_part:
+            for k, v in t.items():
+                kt_sum[k] = kt_sum.get(k, 0.0) + v
+        launches += len(per_part)
+    eng.set_option(gpu.OPT_KERNEL_TIMING, 0)
+    kt = {k: v / launches for k, v in kt_sum.items()}  # average launch duration (ms)
+    single = mine
     dom = max(kt, key=kt.get)
-    # lane-evaluations each launch processes (SURVEY.md §8(d) units) ...
-    launch_evals = {"k_precheck": 8 * single.ctMPUs, "k_mpu": 512 * single.ctFieldMPUs,
-                    "k_vertex": 4 * single.ctVertices, "k_finish": 4 * single.ctVertices}
+    # lane-evaluations one launch processes, on average (SURVEY.md §8(d) units) ...
+    launch_evals = {"k_precheck": 8 * single.ctMPUs / nstreams, "k_mpu": 512 * fmpus / launches,
+                    "k_vertex": 4 * single.ctVertices / nstreams, "k_finish": 4 * single.ctVertices / nstreams}
     # ... times the fp32 ops per lane-evaluation of that stage that the reference executes on
     # this input (its own op-box pruning included; the oracle's counters priced by
     # parsip_amd/costmodel.py, tests/golden/workload_ops.json); else the unpruned figure
@@ -325,22 +335,23 @@ def main():
         per_eval, per_src = wops[dom] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
     alg_ops = launch_evals[dom] * per_eval
     achieved = alg_ops / (kt[dom] * 1e-3) / 1e12
+    prof_ok = args.config == "C3" and grp.world == 1 and nstreams == 2 and args.jit == 1
     pmc, pmc_src = committed_profile("pmc")
-    pe = profile_entry(pmc, dom, args.jit) if args.config == "C3" and grp.world == 1 else None
+    pe = profile_entry(pmc, dom, args.jit) if prof_ok else None
     tr, tr_src = committed_profile("traffic")
-    te = profile_entry(tr, dom, args.jit) if args.config == "C3" and grp.world == 1 else None
+    te = profile_entry(tr, dom, args.jit) if prof_ok else None
     roof = {"bound": "valu", "pipe": "fp32 VALU (no MFMA: scalar field evaluation; SURVEY.md §8(d))",
             "kernel": dom, "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
             "traffic": round(te["traffic_bytes"]) if te and "traffic_bytes" in te else None,
             "traffic_source": tr_src if te else None,
-            "kernel_ms": round(kt[dom], 4), "lane_evals": launch_evals[dom], "ops_per_eval": round(per_eval, 1),
-            "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
-            "note": "achieved = lane-evaluations this launch performs x the reference's fp32 ops per "
-                    "evaluation / hipEvent launch time, on a single-stream run of the rank's whole range (the "
-                    "timed steps run it as `streams` parts); exact per-wave culling skips part of those ops, "
-                    "so valu_issue (executed VALU instructions x 2 cycles per wave64 on SIMD-32, PMC) is the "
-                    "hardware-side utilisation"}
+            "kernel_ms": round(kt[dom], 4), "launches_timed": launches, "lane_evals": round(launch_evals[dom]),
+            "ops_per_eval": round(per_eval, 1), "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
+            "note": "per launch: achieved = the lane-evaluations one launch performs (k_mpu: 512 x S2-evaluated "
+                    "MPUs of its part) x the reference's fp32 ops per evaluation / its hipEvent duration, "
+                    "averaged over the parts and repetitions of the timed engine; exact per-wave culling skips "
+                    "part of those ops, so valu_issue (executed VALU instructions x 2 cycles per wave64 on "
+                    "SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side utilisation"}
     if pe and "SQ_INSTS_VALU" in pe:
         roof["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (kt[dom] * 1e-3 * 2.4e9 * 1024), 4)
         roof["valu_source"] = pmc_src
@@ -359,7 +370,7 @@ def main():
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: C3 BlobTree from std::mt19937(42) as in the reference probe (SURVEY.md §6, §8(d))",
+        "data": f"synthetic: {args.config} BlobTree from std::mt19937(42) as in the reference probe (SURVEY.md §6, §8(d))",
         "config": {"workload": (f"{args.config}: {model.ct_prims}-prim/{model.ct_ops}-op BlobTree, {N}^3 cells, "
                                 f"{n_mpus} MPUs")
                                + (" split over the ranks (C4)" if full is not None else "")
@@ -372,7 +383,7 @@ def main():
                    else "interpreter (jit unavailable)", "set_model_s": round(t_model, 4),
                    "jit_ready_s": round(t_jit, 3)},
         "roofline": roof,
-        "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+        "kernel_ms_per_launch": {k: round(v, 4) for k, v in kt.items()},
         "mesh": {"vertices": info.ctVertices, "triangles": info.ctTriangles, "passed_s1": info.ctPassedPrecheck,
                  "surface_mpus": info.ctSurfaceMPUs, "field_mpus": info.ctFieldMPUs, "per_rank": counts},
         "hbm_gbs_algorithmic": round((mine.ctVertices * 36 + mine.ctTriangles * 12) / (ms_step * 1e-3) / 1e9, 2),

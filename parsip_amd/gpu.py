@@ -348,10 +348,8 @@ class Polygonizer:
         return out
 
     def kernel_times(self) -> dict:
-        ms = (ctypes.c_float * 8)()
-        names = (ctypes.c_char_p * 8)()
-        n = self._L.psgpu_last_kernel_times(self._ctx, ms, 8, names)
-        return {names[i].decode(): ms[i] for i in range(n)}
+        """Per-kernel hipEvent times (ms) of the last finished run (OPT_KERNEL_TIMING)."""
+        return _kernel_times(self._L, self._ctx)
 
     def field_values(self, xyz: np.ndarray, mode: int = 0):
         """mode 0: quads of consecutive points; 1: per point; 2: per point + colour."""
@@ -474,6 +472,17 @@ class Group:
 
     def context_ptr(self, part: int):
         return self._L.psgpu_group_context(self._g, part)
+
+    def kernel_times(self, part: int) -> dict:
+        """Per-kernel hipEvent times (ms) of part `part` in the last finished run."""
+        return _kernel_times(self._L, ctypes.c_void_p(self.context_ptr(part)))
+
+
+def _kernel_times(L, ctx) -> dict:
+    ms = (ctypes.c_float * 8)()
+    names = (ctypes.c_char_p * 8)()
+    n = L.psgpu_last_kernel_times(ctx, ms, 8, names)
+    return {names[i].decode(): ms[i] for i in range(n)}
 
 
 def comm_unique_id() -> bytes:

@@ -1,8 +1,8 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, the bench line, a kernel-trace profile of the
-# same bench command, and PMC passes (FETCH_SIZE, WRITE_SIZE, VALU mix) for the HBM traffic
-# and issue rate.  Every GPU step has its own time limit; the first failure ends the script.
-# Usage (from the repo root, on the box): bash tools/gpu_round.sh TAG
+# One GPU-box session: parity tests, smoke, a kernel-trace profile of the bench command, PMC
+# passes (FETCH_SIZE, WRITE_SIZE; instruction mix, stalls, occupancy), then the bench lines
+# (C3 headline, C5 frame).  Every GPU step has its own time limit; the first failure ends the
+# script.  Usage (from the repo root, on the box): bash tools/gpu_round.sh TAG [notests]
 # Only gpurun_out/ comes back from the box: afterwards, here, run
 #   bash tools/gpu_round.sh TAG --collect
 # to copy the summaries into profiles/.
@@ -10,25 +10,32 @@ set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 if [ "$2" = "--collect" ]; then
-  cp $OUT/kt/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv && cp $OUT/traffic.json profiles/${TAG}_traffic.json &&
-  cp $OUT/valu.json profiles/${TAG}_valu.json && cp $OUT/bench.json profiles/${TAG}_bench.json
-  exit $?
+  for f in kernel_stats.csv traffic.json pmc.json bench.json bench_c5.json; do
+    src=$OUT/$f; [ $f = kernel_stats.csv ] && src=$OUT/kt/run_kernel_stats.csv
+    [ $f = pmc.json ] && src=$OUT/pmc/pmc.json
+    [ -f $src ] && cp $src profiles/${TAG}_$f
+  done
+  exit 0
 fi
 mkdir -p $OUT profiles
 export TMPDIR=/tmp
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
-tail -2 $OUT/gpu_tests.log
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
-cat $OUT/smoke.log
+if [ "$2" != "notests" ]; then
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+  tail -2 $OUT/gpu_tests.log
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+  cat $OUT/smoke.log
+fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --no-cpu > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES --output-format csv -d $OUT/valu -o run -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $OUT/valu.log 2>&1 || { tail -20 $OUT/valu.log; exit 1; }
-python3 tools/valu.py $OUT/valu > $OUT/valu.json && cp $OUT/valu.json profiles/${TAG}_valu.json || exit 1
 python3 tools/traffic.py $OUT > $OUT/traffic.json && cp $OUT/traffic.json profiles/${TAG}_traffic.json || exit 1
-cp $(find $OUT/kt -name '*kernel_stats.csv' | head -1) profiles/${TAG}_kernel_stats.csv
+bash tools/pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+cp $OUT/pmc/pmc.json profiles/${TAG}_pmc.json || exit 1
+cp $OUT/kt/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
 cat $OUT/traffic.json
-# the bench line, measured after the profiles so it reports their traffic / VALU figures
+# the bench lines, measured after the profiles so they report their traffic / VALU figures
 timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cp $OUT/bench.json profiles/${TAG}_bench.json
 cat $OUT/bench.json
+timeout -k 10 300 python3 bench.py --config C5 --no-cpu --steps 50 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -20 $OUT/bench_c5.err; exit 1; }
+cat $OUT/bench_c5.json

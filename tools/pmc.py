@@ -18,7 +18,7 @@ dur = collections.defaultdict(list)
 for p in glob.glob(os.path.join(d, "p*", "**", "*kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(p)):
         dur[r["Kernel_Name"].split("(")[0]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-out = {"note": "per launch; valu_issue = SQ_INSTS_VALU x 2 cyc / (us x 2400 x 1024 SIMDs); SQ_*_CYCLES and "
+out = {"note": "per launch; mean_waves_per_simd = SQ_WAVE_CYCLES x 4 / (us x 2400 x 1024); valu_issue = SQ_INSTS_VALU x 2 cyc / (us x 2400 x 1024 SIMDs); SQ_*_CYCLES and "
                "SQ_WAIT_* count quad-cycles (MI355X_MICROARCH.md); profiled clocks run lower than un-profiled",
        "kernels": {}}
 for k, c in acc.items():
@@ -37,5 +37,7 @@ for k, c in acc.items():
                 e["share_" + n[3:].lower()] = round(e[n] / wc, 3)
     if e.get("SQ_WAVES") and wc:
         e["quad_cycles_per_wave"] = round(wc / e["SQ_WAVES"], 1)
+    if wc and e.get("median_us_profiled"):  # occupancy: resident waves per SIMD, time-averaged
+        e["mean_waves_per_simd"] = round(wc * 4 / (e["median_us_profiled"] * 2400 * 1024), 2)
     out["kernels"][k] = e
 print(json.dumps(out, indent=1))

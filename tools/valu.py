@@ -13,7 +13,7 @@ for p in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv"), r
     for r in csv.DictReader(open(p)):
         acc[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {"note": "per launch, averaged over the profiled launches; VALU issue utilisation = "
-               "SQ_INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs)", "kernels": {}}
+               "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (kernel time x 2.4 GHz x 1024 SIMDs)", "kernels": {}}
 for k, d in acc.items():
     if "rocclr" in k or "__amd" in k:
         continue
