@@ -611,10 +611,10 @@ __device__ __forceinline__ void stamp_end(const Params& p, int K, uint64_t t0, u
         r[2] = (uint64_t)item | ((uint64_t)((hw & 0xffffu) | (xcc << 16)) << 32);
     }
 }
-// Phase stamps inside one wave (debug bit 4096, k_mpu): 8 words per wave after the
-// kernels' records; phase 0 = entry.
-__device__ __forceinline__ void phase_stamp(const Params& p, int ph) {
-    if (!(p.debug & 4096u) || !p.stamps) return;
+// Phase stamps inside one wave (debug bit 4096: k_mpu, 8192: k_precheck): 8 words per
+// wave after the kernels' records; phase 0 = entry.
+__device__ __forceinline__ void phase_stamp(const Params& p, int ph, uint32_t bit = 4096u) {
+    if (!(p.debug & bit) || !p.stamps) return;
     const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w >= p.stampCap) return;
     const uint64_t t = stamp_now();
@@ -651,16 +651,18 @@ template <class EV>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
+    phase_stamp(p, 0, 8192u);
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
     CullLanes cl;  // loaded first: independent of everything below
     if (p.cull) cl = load_cull_lanes(as_const(p.model));
-    const uint32_t W = blockIdx.x * 4u + (uint32_t)wave;
+    const uint32_t W = blockIdx.x * 4u + (uint32_t)wave;  // wave slot: decides the queue shard
     const uint32_t bzN = p.brickDims[2], byN = p.brickDims[1];
     const uint32_t nBricks = p.brickDims[0] * byN * bzN;
+    const uint32_t B = W < nBricks ? (uint32_t)(((uint64_t)W * p.brickStride) % nBricks) : W;  // its brick
     const uint32_t g = (uint32_t)lane >> 3;
-    const uint32_t mi = 2u * (p.brickI0 + W / (byN * bzN)) + ((g >> 2) & 1u);
-    const uint32_t mj = 2u * ((W / bzN) % byN) + ((g >> 1) & 1u);
-    const uint32_t mk = 2u * (W % bzN) + (g & 1u);
+    const uint32_t mi = 2u * (p.brickI0 + B / (byN * bzN)) + ((g >> 2) & 1u);
+    const uint32_t mj = 2u * ((B / bzN) % byN) + ((g >> 1) & 1u);
+    const uint32_t mk = 2u * (B % bzN) + (g & 1u);
     const uint32_t mg = (mi * p.dims[1] + mj) * p.dims[2] + mk;
     const bool valid = W < nBricks && mi < p.dims[0] && mj < p.dims[1] && mk < p.dims[2] && mg >= p.mpuBegin &&
                        mg - p.mpuBegin < p.mpuCount;
@@ -682,6 +684,13 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
         f = (float)(cm.lo & 1ull) - 1.0f;
     }
     const uint64_t bal = ballot(valid && f > 0.0f);
+    phase_stamp(p, 1, 8192u);
+    if ((p.debug & 8192u) && p.stamps && lane == 0) {  // phase word 7: the wave's live primitives, S1 passes
+        const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (w < p.stampCap)
+            p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)w + 7] =
+                (uint64_t)(128 - __popcll(cm.lo) - __popcll(cm.hi)) | ((uint64_t)__popcll(bal) << 16);
+    }
     uint32_t flags8 = 0;  // bit g: MPU of lanes 8g..8g+7 passed
 #pragma unroll
     for (int q = 0; q < 8; ++q) flags8 |= (((bal >> (8 * q)) & 0xffull) != 0ull ? 1u : 0u) << q;
@@ -713,6 +722,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
             proven8 |= (all ? 1u : 0u) << q;
         }
         proven8 &= flags8;
+        phase_stamp(p, 2, 8192u);
     }
     const uint32_t queue8 = flags8 & ~proven8;
     // lane g < 8 speaks for MPU g (its values are those of lane 8g)
@@ -732,6 +742,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(queue8));
     base = lane_value(base, 0);
     if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u))] = mOf;
+    phase_stamp(p, 3, 8192u);
     // Culling masks of each queued MPU, from this wave's culling segments (already in
     // registers): its box for S2 (with the queue entry: k_mpu loads no culling data) and the
     // box grown by the normal delta for k_vertex / k_finish

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -414,6 +415,15 @@ void brick_layout(const psgpu_ctx* c, uint32_t* i0, uint32_t bd[3]) {
     bd[1] = (c->dims[1] + 1) / 2;
     bd[2] = (c->dims[2] + 1) / 2;
 }
+// The brick permutation of k_precheck: stride 1 keeps the lattice order; otherwise a
+// stride near n / golden ratio, coprime with n, so consecutive wave slots (one block, one
+// CU) take bricks far apart and the bricks crossed by the surface spread over the chip.
+uint32_t brick_stride(uint32_t n, bool spread) {
+    if (!spread || n < 3) return 1u;
+    for (uint32_t s = (uint32_t)(n * 0.6180339887) | 1u; s > 1; --s)
+        if (std::gcd(s, n) == 1u) return s;
+    return 1u;
+}
 size_t brick_count(const psgpu_ctx* c) {
     uint32_t i0, bd[3];
     brick_layout(c, &i0, bd);
@@ -455,6 +465,7 @@ Params make_params(psgpu_ctx* c) {
     p.cull = (uint32_t)c->cull;
     brick_layout(c, &p.brickI0, p.brickDims);
     p.preBlocks = (uint32_t)((brick_count(c) + 3) / 4);
+    p.brickStride = brick_stride((uint32_t)brick_count(c), (c->debug & 16384) != 0);
     p.pq = c->pq;
     p.pqMask = c->pqMask;
     p.pShardCap = c->pShardCap;

@@ -200,6 +200,8 @@ struct Params {
     uint32_t preBlocks;     // k_precheck blocks (4 waves, one 2x2x2 brick of MPUs per wave)
     uint32_t brickI0;       // first brick row (x) touching the MPU range
     uint32_t brickDims[3];  // bricks of the range along x, y, z
+    uint32_t brickStride;   // wave W takes brick (W * brickStride) mod bricks (coprime: a
+                            // permutation that spreads the surface's heavy bricks over the CUs)
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
     uint64_t* pqMask;       // per queue entry: the MPU box's culling mask (2 words, by k_precheck)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow

@@ -116,7 +116,57 @@ def mpu_phases(config="C3"):
     print(f"  wave entry time: median {np.median(st):.2f} us, p90 {np.percentile(st, 90):.2f}, max {st.max():.2f}")
 
 
+def precheck_phases(config="C3"):
+    """k_precheck phase stamps (debug bit 8192): per wave, entry -> S1 walk done, -> field
+    bounds done (waves holding a survivor), -> queue append, -> end (culling masks)."""
+    model, cs, N = synth.make_config(config)
+    p = gpu.Polygonizer(0)
+    p.set_model(model)
+    for _ in range(3):
+        p.run(cs)
+    p.set_option(gpu.OPT_STAMPS, 1 << 17)
+    p.set_option(gpu.OPT_DEBUG, 8192)
+    p.run(cs)
+    S = p.stamps()
+    rec = S["k_precheck"].astype(np.int64)
+    n = len(rec)
+    ph = S["mpu_phases"].astype(np.int64)[:n]
+    t0 = rec[:, 0].min()
+    life = (rec[:, 1] - rec[:, 0]) * TICK_US
+    heavy = ph[:, 2] != 0
+    print(f"k_precheck waves {n}, with survivors (bounded) {int(heavy.sum())}")
+    for nm, sel in (("all", np.ones(n, bool)), ("bounded", heavy), ("no survivor", ~heavy)):
+        if not sel.any():
+            continue
+        s1 = (ph[sel, 1] - ph[sel, 0]) * TICK_US
+        print(f"  {nm:12s} life p50 {np.median(life[sel]):6.2f} p90 {np.percentile(life[sel], 90):6.2f} "
+              f"max {life[sel].max():6.2f} | S1 walk p50 {np.median(s1):6.2f} max {s1.max():6.2f}")
+    if heavy.any():
+        b = (ph[heavy, 2] - ph[heavy, 1]) * TICK_US
+        q = (ph[heavy, 3] - ph[heavy, 2]) * TICK_US
+        e = (rec[heavy, 1] - ph[heavy, 3]) * TICK_US
+        print(f"  bounded: bound p50 {np.median(b):.2f} max {b.max():.2f} | queue p50 {np.median(q):.2f} "
+              f"max {q.max():.2f} | masks p50 {np.median(e):.2f} max {e.max():.2f}")
+        live = ph[:, 7] & 0xFFFF
+        live = live - (128 - model.ct_prims)  # primitives of the tree not culled for the wave
+        s1 = (ph[:, 1] - ph[:, 0]) * TICK_US
+        for lo, hi in ((0, 1), (1, 4), (4, 8), (8, 16), (16, 24), (24, 33)):
+            sel = (live >= lo) & (live < hi)
+            if sel.any():
+                print(f"  live prims [{lo},{hi}): waves {int(sel.sum()):5d}  S1 walk p50 {np.median(s1[sel]):6.2f} "
+                      f"max {s1[sel].max():6.2f}  life p50 {np.median(life[sel]):6.2f} max {life[sel].max():6.2f}")
+        worst = np.argsort(life)[-10:]
+        for w in worst:
+            print(f"  worst wave {w} (live prims {int(live[w])}): start {(rec[w, 0] - t0) * TICK_US:.2f} life {life[w]:.2f} | "
+                  + " ".join(f"{(ph[w, i + 1] - ph[w, i]) * TICK_US:.2f}" if ph[w, i + 1] else "-" for i in range(3))
+                  + f" | end {(rec[w, 1] - ph[w, 3]) * TICK_US if ph[w, 3] else -1:.2f}")
+
+
 if __name__ == "__main__":
+    if "--precheck" in sys.argv:
+        sys.argv.remove("--precheck")
+        precheck_phases()
+        sys.exit(0)
     if "--phases" in sys.argv:
         mpu_phases()
     else:
