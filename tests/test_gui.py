@@ -1,0 +1,226 @@
+"""Compat mode ("GUI-path semantics"): ParsipHaptics' own polygonizer,
+CParsipOptimized over a COMPACTBLOBTREE, on the MI355X library against its CPU
+restatement (oracle/psgui.c).
+
+CPU tests: the tree conversion (COMPACTBLOBTREE::convert), the oracle's own invariants,
+the MC-table property the device's vertex-ownership rule rests on, the libm agreement of
+the correctly rounded powf / cosf / sinf, and the consistency of the reference scene with
+the one run the reference recorded (Distrib/ParsipHaptics_Release.csv).
+GPU tests (-m gpu): bit-exact meshes, statistics and field probes on the reference's
+train scene and on random trees with every supported node type.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import psgui
+from gui_util import assert_gui_mesh_equal, bits, random_tree
+from parsip_amd import blobtree as bt
+from parsip_amd import gui, scene
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENE = os.path.join(ROOT, "tests", "golden", "train_corrected.scene")
+B = bt.BlobNodeType
+
+
+@pytest.fixture(scope="module")
+def train():
+    root = scene.load_scene(SCENE)[0]
+    code, tree = gui.compact_blobtree(root)
+    assert code == 0
+    return root, tree
+
+
+# ---------------------------------------------------------------- CPU --------
+def test_convert_train_scene(train):
+    root, tree = train
+    assert (tree.ct_prims, tree.ct_ops) == (95, 31)  # recursive_CountPrimitives / Operators
+    assert len(tree.kids) == 125  # every node but the root is some operator's kid
+    # pre-order operator ids: kids of op i that are operators have larger ids
+    for i, o in enumerate(tree.ops):
+        for k in tree.kids[o["kidStart"]:o["kidStart"] + o["ctKids"]]:
+            if k >> 16:
+                assert (k & 0xFFFF) > i
+    # a matrix slot per primitive with a non-identity backward matrix (:266-283)
+    assert len(tree.mtx) == 1 + int(np.count_nonzero(tree.prims["idxMtx"]))
+    assert np.array_equal(tree.mtx[0]["r"], np.eye(4, dtype=np.float32))
+    ricci = tree.ops[tree.ops["type"] == B.OP_RICCIBLEND]
+    assert len(ricci) and np.all(ricci["params"][:, 1] == np.float32(1.0) / ricci["params"][:, 0])
+
+
+def test_convert_errors():
+    assert gui.compact_blobtree(None)[0] == gui.ERR_PARAM_ERROR
+    bad = bt.Op(B.OP_UNION, bt.Point((0, 0, 0)), bt.BlobNode(B.PRIM_POLYGON))
+    assert gui.compact_blobtree(bad)[0] == gui.ERR_NODE_NOT_RECOGNIZED
+    bad = bt.Op(B.OP_UNION, bt.Op(B.OP_GRADIENTBLEND, bt.Point((0, 0, 0)), bt.Point((1, 0, 0))))
+    assert gui.compact_blobtree(bad)[0] == gui.ERR_NODE_NOT_RECOGNIZED
+    many = bt.Op(B.OP_BLEND, *[bt.Point((0.01 * i, 0, 0)) for i in range(1025)])
+    assert gui.compact_blobtree(many)[0] == gui.ERR_KIDS_OVERFLOW
+
+
+def test_mc_table_crossing_edges_are_listed():
+    """The device numbers vertices by the first cell (loop order) that holds their edge: that
+    needs every config's triangle list to name exactly its sign-change edges."""
+    import psoracle
+
+    tri = np.asarray(psoracle.tritable()).reshape(256, 16)
+    c1, c2 = [0, 2, 0, 1, 4, 6, 4, 5, 0, 1, 2, 3], [1, 3, 2, 3, 5, 7, 6, 7, 4, 5, 6, 7]
+    for cfg in range(256):
+        crossing = {e for e in range(12) if ((cfg >> c1[e]) & 1) != ((cfg >> c2[e]) & 1)}
+        assert {int(e) for e in tri[cfg] if e != -1} == crossing, cfg
+
+
+def test_oracle_vertices_on_surface_and_closed(train):
+    _, tree = train
+    r = psgui.polygonize(tree, *tree.root_octree, 0.2, 0.5, threads=8)
+    i = r.info
+    assert i.ctVertices == len(r.pos) > 1000 and i.ctTriangles == len(r.tris)
+    assert i.ctMPUs == i.ctIntersectedMPUs <= i.ctProcessedMPUs <= i.ctLatticeMPUs
+    f, _ = psgui.field_values(tree, r.pos)
+    converged = np.abs(f - 0.5) < 0.001
+    assert converged.mean() > 0.97  # the rest ran out of the 8 Newton iterations (reference behaviour)
+    # per MPU the triangles index that MPU's vertices only; normals are unit
+    for m in np.nonzero(r.stats["ctTriangles"])[0][:50]:
+        t = r.tris[r.mpu_t[m]:r.mpu_t[m + 1]]
+        assert t.min() >= r.mpu_v[m] and t.max() < r.mpu_v[m + 1]
+    # unit normals, or normalizeXYZ's (1, 1, 1) where Newton ended on a flat field (:1072-1087)
+    unit = np.isclose(np.linalg.norm(r.nrm, axis=1), 1.0, atol=1e-5)
+    assert np.all(unit | np.all(r.nrm == 1.0, axis=1)) and unit.mean() > 0.97
+    assert i.ctFieldEvals == int(r.stats["fieldEvals"].sum())
+    assert i.ctCellsInIntersectedMPUs == 343 * i.ctIntersectedMPUs
+
+
+def test_correctly_rounded_libm_against_glibc(train):
+    """The documented deviation (oracle/psgui.c header): Ricci's powf and the warps' cosf / sinf
+    are the correctly rounded fp32 results on both sides.  The host libm the reference would
+    link differs from them by at most 1 ulp, on a small share of this scene's arguments (Ricci:
+    kid fields in [0, 1] to the powers 2, 16, 20 and back) and of random angles."""
+    _, tree = train
+    r = psgui.polygonize(tree, *tree.root_octree, 0.25, 0.5, threads=8)
+    ricci = tree.ops[tree.ops["type"] == B.OP_RICCIBLEND]
+    f = np.concatenate([np.linspace(0, 1, 20001, dtype=np.float32), np.abs(r.pos[:, 0] % 1)]).astype(np.float32)
+    n_pow, n = 0, 0
+    for nn, inv in ricci["params"][:, :2]:
+        for e in (nn, inv):
+            d, u = psgui.libm_agreement(f, np.full(len(f), e, np.float32))
+            assert u[0] <= 1, (e, u)
+            n_pow += int(d[0])
+            n += len(f)
+    ang = np.random.default_rng(1).uniform(-8, 8, 200000).astype(np.float32)
+    d, u = psgui.libm_agreement(ang, ang)
+    assert u[1] <= 1 and u[2] <= 1, u
+    assert n_pow / n < 0.01 and d[1] / len(ang) < 0.03 and d[2] / len(ang) < 0.03, (n_pow / n, d)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_random_trees_convert_and_run(seed):
+    code, tree = gui.compact_blobtree(random_tree(seed))
+    assert code == 0
+    r = psgui.polygonize(tree, *tree.root_octree, 0.08, 0.5, threads=8)
+    assert r.info.ctTriangles > 0 and np.all(np.isfinite(r.pos))
+
+
+def test_reference_csv_consistency(train):
+    """The only output the reference recorded for this path (Distrib/ParsipHaptics_Release.csv:2,
+    95 prims, cellsize 0.13) came from a build with GRID_DIM 16 and a scene with 95 operators
+    (train_corrected has 31): not a parity pin.  The restatement at GRID_DIM 16
+    on the shipped scene stays within 2 % of its mesh and crossed-cell counts."""
+    _, tree = train
+    r = psgui.polygonize(tree, *tree.root_octree, 0.13, 0.5, threads=8, grid_dim=16)
+    ref = {"faces": 146352, "vertices": 82370, "cells": 72620}
+    got = {"faces": r.info.ctTriangles, "vertices": r.info.ctVertices, "cells": r.info.ctIntersectedCells}
+    for k in ref:
+        assert abs(got[k] - ref[k]) / ref[k] < 0.02, (k, got[k], ref[k])
+
+
+# ---------------------------------------------------------------- GPU --------
+@pytest.fixture(scope="module")
+def gui_ctx():
+    from parsip_amd import gpu
+
+    gpu.load()
+    assert gpu.device_count() > 0, "no HIP device visible: GPU tests must run on an MI355X"
+    p = gui.ParsipOptimized(0)
+    yield p
+    p.close()
+
+
+def _both(ctx, tree, cs, iso=0.5, octree=None):
+    lo, hi = octree if octree is not None else tree.root_octree
+    ctx.setup(tree, (lo, hi), 0, cs, iso)
+    ctx.run()
+    gm = ctx.exportMesh()
+    om = psgui.polygonize(tree, lo, hi, cs, iso, threads=8)
+    return gm, om
+
+
+def _info_equal(a, b):
+    for f, _ in gui.PsGuiInfo._fields_:
+        va, vb = getattr(a, f), getattr(b, f)
+        if f == "dims":
+            va, vb = list(va), list(vb)
+        assert va == vb, (f, va, vb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cs", [0.25, 0.13])
+def test_gpu_train_scene_bit_exact(gui_ctx, train, cs):
+    _, tree = train
+    gm, om = _both(gui_ctx, tree, cs)
+    _info_equal(gui_ctx.finish(), om.info)
+    assert_gui_mesh_equal(gm, om, f"train cs={cs}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_gpu_random_trees_bit_exact(gui_ctx, seed):
+    code, tree = gui.compact_blobtree(random_tree(seed))
+    assert code == 0
+    gm, om = _both(gui_ctx, tree, 0.06)
+    _info_equal(gui_ctx.finish(), om.info)
+    assert_gui_mesh_equal(gm, om, f"seed {seed}")
+
+
+@pytest.mark.gpu
+def test_gpu_field_and_colour_probe(gui_ctx, train):
+    _, tree = train
+    gui_ctx.set_tree(tree)
+    lo, hi = tree.root_octree
+    xyz = np.random.default_rng(5).uniform(lo, hi, size=(20000, 3)).astype(np.float32)
+    gf, gc = gui_ctx.field_values(xyz)
+    of, oc = psgui.field_values(tree, xyz)
+    assert np.array_equal(bits(gf), bits(of)) and np.array_equal(bits(gc), bits(oc))
+    assert np.count_nonzero(gf) > 1000
+
+
+@pytest.mark.gpu
+def test_gpu_isovalue_and_empty_lattice(gui_ctx, train):
+    _, tree = train
+    gm, om = _both(gui_ctx, tree, 0.3, iso=0.3)
+    assert_gui_mesh_equal(gm, om, "iso 0.3")
+    far = (np.array([100, 100, 100], np.float32), np.array([101, 101, 101], np.float32))
+    gm, om = _both(gui_ctx, tree, 0.3, octree=far)
+    assert len(gm.pos) == 0 and gui_ctx.finish().ctProcessedMPUs == 0 == om.info.ctProcessedMPUs
+
+
+@pytest.mark.gpu
+def test_gpu_rejects_unsupported_nodes(gui_ctx):
+    pcm = bt.Op(B.OP_PCM, bt.Point((0, 0, 0)), bt.Point((0.5, 0, 0)))
+    code, tree = gui.compact_blobtree(pcm)
+    assert code == 0
+    from parsip_amd import gpu
+
+    with pytest.raises(gpu.PsgpuError) as e:
+        gui_ctx.set_tree(tree)
+    assert e.value.code == gui.RET_UNSUPPORTED
+
+
+@pytest.mark.gpu
+def test_gpu_run_polygonizer_api(train):
+    root, _ = train
+    p = gui.Run_Polygonizer(root, 0.25)
+    V, T = p.statsMeshInfo()
+    assert V > 0 and T > 0 and p.countMPUs() == p.statsIntersectedMPUs()
+    assert p.statsTotalCellsInIntersectedMPUs() == 343 * p.statsIntersectedMPUs()
+    p.close()

@@ -28,7 +28,9 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert set(gpu.EXPORTED_SYMBOLS) == set(names)
+    from parsip_amd import gui
+
+    assert set(gpu.EXPORTED_SYMBOLS) | set(gui.EXPORTED_SYMBOLS) == set(names)
 
 
 def test_version_string():
