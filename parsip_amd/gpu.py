@@ -337,15 +337,7 @@ class Polygonizer:
     def stamps(self) -> dict:
         """Per-wave timeline of the last run (OPT_STAMPS): kernel -> (waves, 3) uint64 array
         of start, end (100 MHz ticks), item | hw id << 32, launched waves only."""
-        cap = ctypes.c_uint32()
-        _check(self._L.psgpu_download_stamps(self._ctx, None, ctypes.byref(cap)), "psgpu_download_stamps")
-        n = max(cap.value, 1)
-        raw = np.zeros(len(STAMP_KERNELS) * n * 3 + n * 8, np.uint64)
-        _check(self._L.psgpu_download_stamps(self._ctx, raw.ctypes.data, ctypes.byref(cap)), "psgpu_download_stamps")
-        buf = raw[:len(STAMP_KERNELS) * n * 3].reshape(len(STAMP_KERNELS), n, 3)
-        out = {k: buf[i][buf[i][:, 0] != 0] for i, k in enumerate(STAMP_KERNELS)}
-        out["mpu_phases"] = raw[len(STAMP_KERNELS) * n * 3:].reshape(n, 8)
-        return out
+        return _stamps(self._L, self._ctx)
 
     def kernel_times(self) -> dict:
         """Per-kernel hipEvent times (ms) of the last finished run (OPT_KERNEL_TIMING)."""
@@ -476,6 +468,32 @@ class Group:
     def kernel_times(self, part: int) -> dict:
         """Per-kernel hipEvent times (ms) of part `part` in the last finished run."""
         return _kernel_times(self._L, ctypes.c_void_p(self.context_ptr(part)))
+
+    def stamps(self, part: int) -> dict:
+        """The per-wave timeline (OPT_STAMPS) of part `part` in the last finished run."""
+        return _stamps(self._L, ctypes.c_void_p(self.context_ptr(part)))
+
+
+def _stamps(L, ctx) -> dict:
+    cap = ctypes.c_uint32()
+    _check(L.psgpu_download_stamps(ctx, None, ctypes.byref(cap)), "psgpu_download_stamps")
+    n = max(cap.value, 1)
+    raw = np.zeros(len(STAMP_KERNELS) * n * 3 + n * 8, np.uint64)
+    _check(L.psgpu_download_stamps(ctx, raw.ctypes.data, ctypes.byref(cap)), "psgpu_download_stamps")
+    buf = raw[:len(STAMP_KERNELS) * n * 3].reshape(len(STAMP_KERNELS), n, 3)
+    out = {k: buf[i][buf[i][:, 0] != 0] for i, k in enumerate(STAMP_KERNELS)}
+    out["mpu_phases"] = raw[len(STAMP_KERNELS) * n * 3:].reshape(n, 8)
+    return out
+
+
+def kernel_spans(stamps: dict) -> dict:
+    """Per kernel, first wave start -> last wave end (ms, device clock) of one run."""
+    out = {}
+    for k in STAMP_KERNELS:
+        st = stamps.get(k)
+        if st is not None and len(st):
+            out[k] = float(int(st[:, 1].max()) - int(st[:, 0].min())) * 1e-5  # 100 MHz ticks -> ms
+    return out
 
 
 def _kernel_times(L, ctx) -> dict:
