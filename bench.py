@@ -178,6 +178,68 @@ def cpu_baseline(model, cs, n_cells):
             "cpu_model": cpu_model, "nproc": os.cpu_count(), "smt_active": smt}
 
 
+class Engine:
+    """One device context over the rank's MPU range [begin, end) (parts == 1), or a group of
+    `parts` cost-balanced sub-ranges on as many streams of the device."""
+
+    def __init__(self, device, model, cs, args, begin, end, costs, poly=None):
+        self.cs, self.begin, self.end, self.parts = cs, begin, end, max(1, args.parts)
+        self.comm = None
+        self.owns = poly is None
+        if self.parts == 1:
+            self.p = poly if poly is not None else gpu.Polygonizer(device)
+            self.obj = self.p
+        else:
+            self.p = None
+            self.obj = gpu.Group([device] * self.parts)
+        if poly is None or self.parts > 1:
+            if args.no_cull:
+                self.obj.set_option(gpu.OPT_CULLING, 0)
+            self.obj.set_option(gpu.OPT_JIT, args.jit)
+            if args.debug:
+                self.obj.set_option(gpu.OPT_DEBUG, args.debug)
+            self.obj.set_model(model)
+        if self.parts > 1:
+            self.obj.set_split(gpu.split_costs(costs[begin:end], self.parts, begin))
+
+    def polygonize(self):
+        if self.p is not None:
+            self.p.polygonize(self.cs, self.begin, self.end)
+        else:
+            self.obj.polygonize(self.cs)
+        if self.comm:
+            self.comm.exchange()
+
+    def finish(self):
+        """(totals, parts) of the last run: over all ranks when exchanging."""
+        if self.comm:
+            return self.comm.result()
+        if self.p is not None:
+            return self.p.finish(), None
+        return self.obj.finish()
+
+    def local_info(self):
+        return self.p.finish() if self.p is not None else self.obj.finish()[0]
+
+    def set_option(self, opt, val):
+        self.obj.set_option(opt, val)
+
+    def launch_times(self):
+        """Per part of the last run: (hipEvent ms per kernel, device-clock spans, S2 MPUs)."""
+        if self.p is not None:
+            info = self.p.finish()
+            return [(self.p.kernel_times(), gpu.kernel_spans(self.p.stamps()), info.ctFieldMPUs)]
+        _, parts = self.obj.finish()
+        return [(self.obj.kernel_times(i), gpu.kernel_spans(self.obj.stamps(i)), parts[i].info.ctFieldMPUs)
+                for i in range(self.parts)]
+
+    def close(self):
+        if self.comm:
+            self.comm.close()
+        if self.p is None or self.owns:
+            self.obj.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,9 +248,12 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="N>1: strong (default: one grid split over the ranks) or weak (a grid per rank)")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="per device: the rank's MPU range as this many cost-balanced parts on as many HIP "
-                         "streams (their kernels overlap each other's tails); 1 = one context")
+    ap.add_argument("--engines", type=int, default=2,
+                    help="per device: this many engines (device contexts, each on its own HIP stream) take the "
+                         "steps in turn; each step is a complete polygonization of the rank's range, queued "
+                         "without host sync, so one run's kernel tails overlap the other's bulk")
+    ap.add_argument("--parts", "--streams", type=int, default=1, dest="parts",
+                    help="per engine: the range as this many cost-balanced parts on as many streams")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
@@ -224,14 +289,13 @@ def main():
     t_jit = time.perf_counter() - t0
     n_mpus = gpu.count_mpus(cs, *model.bbox)
 
-    comm, exchange = None, None
     full = None
     # the cost split: one full planning run on this rank's device (exact results, so every
     # rank computes the same split without communication)
     strong = scaling == "strong" and grp.world > 1
-    nstreams = max(1, args.streams)
+    nparts, neng = max(1, args.parts), max(1, args.engines)
     costs = None
-    if strong or nstreams > 1:
+    if strong or nparts > 1:
         poly.run(cs)
         full = poly.finish()
         costs = poly.mpu_costs()
@@ -241,87 +305,83 @@ def main():
     else:
         begin, end = 0, n_mpus
         full = None
-    eng = poly
-    if nstreams > 1:  # the rank's range as `parts` cost-balanced sub-ranges, one stream each
-        eng = gpu.Group([device] * nstreams)
-        if args.no_cull:
-            eng.set_option(gpu.OPT_CULLING, 0)
-        eng.set_option(gpu.OPT_JIT, args.jit)
-        eng.set_model(model)
-        eng.set_split(gpu.split_costs(costs[begin:end], nstreams, begin))
+    engines = [Engine(device, model, cs, args, begin, end, costs, poly if e == 0 else None) for e in range(neng)]
+    exchange = None
     if strong:
-        if pinned is None:
-            uid = grp.broadcast_bytes(gpu.comm_unique_id() if grp.rank == 0 else None)
-            comm = gpu.Comm(eng, uid, grp.world, grp.rank)
+        if pinned is None:  # one communicator per engine: its all-gathers stay on its stream
+            for e in engines:
+                uid = grp.broadcast_bytes(gpu.comm_unique_id() if grp.rank == 0 else None)
+                e.comm = gpu.Comm(e.obj, uid, grp.world, grp.rank)
             exchange = "rccl all-gather of 8 words per rank per step (library stream)"
         else:
             exchange = "gloo all-gather after the timed steps (ranks share one device: RCCL needs distinct GPUs)"
 
-    def step():
-        if nstreams > 1:
-            eng.polygonize(cs)
-        else:
-            poly.polygonize(cs, begin, end)
-        if comm:
-            comm.exchange()
-
-    def finish():
-        if comm:
-            return comm.result()
-        if nstreams > 1:
-            return eng.finish()
-        return poly.finish(), None
-
-    for _ in range(args.warmup):
-        step()
-        finish()
+    for k in range(max(args.warmup, neng)):
+        engines[k % neng].polygonize()
+    for e in engines:
+        e.finish()
     grp.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    info, _ = finish()
+    for k in range(args.steps):  # step k is one complete polygonization, on engine k mod E
+        engines[k % neng].polygonize()
+    results = [e.finish() for e in engines]
     grp.barrier()
     t1 = time.perf_counter()
     dt = grp.max(t1 - t0)
     ms_step = dt / args.steps * 1e3
     cells_per_step = N ** 3 * (grp.world if scaling == "weak" else 1)
     value = cells_per_step / (ms_step * 1e-3) / 1e6
+    info = results[0][0]
+    mines = [e.local_info() for e in engines]
+    mine = mines[0]
+    if any((m.ctMPUs, m.ctVertices, m.ctTriangles) != (mine.ctMPUs, mine.ctVertices, mine.ctTriangles)
+           for m in mines):
+        sys.exit(f"bench.py rank {grp.rank}: the engines' last runs differ")
 
-    mine = eng.finish()[0] if nstreams > 1 else poly.finish()
     counts = grp.allgather([mine.ctMPUs, mine.ctVertices, mine.ctTriangles])
     check = None
     if full is not None:  # the parts must add up to the full grid of the planning run
         tot = [sum(c[i] for c in counts) for i in range(3)]
         ok = tot == [full.ctMPUs, full.ctVertices, full.ctTriangles]
-        if comm:
+        if engines[0].comm:
             ok = ok and (info.ctMPUs, info.ctVertices, info.ctTriangles) == tuple(tot)
         check = {"parts_sum_to_full_grid": ok, "full": [full.ctMPUs, full.ctVertices, full.ctTriangles]}
         if not ok:
             sys.exit(f"bench.py rank {grp.rank}: parts {counts} do not add up to the full grid {check['full']}")
 
-    # roofline pass: per-kernel hipEvent timing on the library's stream(s), the same engine and
-    # split as the timed steps (each part's kernels on its own stream), so the per-launch
-    # averages are those of a rocprofv3 kernel trace of this command
-    eng.set_option(gpu.OPT_KERNEL_TIMING, 1)
-    eng.set_option(gpu.OPT_STAMPS, 1 << 17)
+    # roofline pass: the same engines run concurrently as in the timed steps; per launch the
+    # device-clock span (first wave start -> last wave end) and the hipEvent bracket, so the
+    # per-launch averages are those of a rocprofv3 kernel trace of this command
+    for e in engines:
+        e.set_option(gpu.OPT_KERNEL_TIMING, 1)
+        e.set_option(gpu.OPT_STAMPS, 1 << 17)
     kt_sum, sp_sum, launches, fmpus = {}, {}, 0, 0
     reps = max(3, min(args.steps, 20))
     for _ in range(reps):
-        if nstreams > 1:
-            _, parts = eng.run(cs)
-            per_part = [(eng.kernel_times(i), gpu.kernel_spans(eng.stamps(i))) for i in range(nstreams)]
-            fmpus += sum(pt.info.ctFieldMPUs for pt in parts)
-        else:
-            fmpus += poly.run(cs, begin, end).ctFieldMPUs
-            per_part = [(poly.kernel_times(), gpu.kernel_spans(poly.stamps()))]
-        for ev, spn in per_part:
-            for k, v in ev.items():
-                kt_sum[k] = kt_sum.get(k, 0.0) + v
+        for e in engines:
+            e.polygonize()
+        for e in engines:
+            for ev, spn, fm in e.launch_times():
+                for k, v in ev.items():
+                    kt_sum[k] = kt_sum.get(k, 0.0) + v
+                for k, v in spn.items():
+                    sp_sum[k] = sp_sum.get(k, 0.0) + v
+                fmpus += fm
+                launches += 1
+    # the same launches with the device to themselves (engine 0 alone): the per-kernel
+    # figure without the other engine's kernels sharing the CUs
+    solo_sum, solo_n, solo_fm = {}, 0, 0
+    for _ in range(reps):
+        engines[0].polygonize()
+        for _, spn, fm in engines[0].launch_times():
             for k, v in spn.items():
-                sp_sum[k] = sp_sum.get(k, 0.0) + v
-        launches += len(per_part)
-    eng.set_option(gpu.OPT_KERNEL_TIMING, 0)
-    eng.set_option(gpu.OPT_STAMPS, 0)
+                solo_sum[k] = solo_sum.get(k, 0.0) + v
+            solo_fm += fm
+            solo_n += 1
+    for e in engines:
+        e.set_option(gpu.OPT_KERNEL_TIMING, 0)
+        e.set_option(gpu.OPT_STAMPS, 0)
+    solo = {k: v / solo_n for k, v in solo_sum.items()}
     ev_ms = {k: v / launches for k, v in kt_sum.items()}  # hipEvent bracket per launch (ms)
     # average launch duration: first wave start -> last wave end on the device clock
     # (s_memrealtime stamps); the hipEvent brackets add the dispatch gap before each kernel
@@ -329,8 +389,8 @@ def main():
     single = mine
     dom = max(kt, key=kt.get)
     # lane-evaluations one launch processes, on average (SURVEY.md §8(d) units) ...
-    launch_evals = {"k_precheck": 8 * single.ctMPUs / nstreams, "k_mpu": 512 * fmpus / launches,
-                    "k_vertex": 4 * single.ctVertices / nstreams, "k_finish": 4 * single.ctVertices / nstreams}
+    launch_evals = {"k_precheck": 8 * single.ctMPUs / nparts, "k_mpu": 512 * fmpus / launches,
+                    "k_vertex": 4 * single.ctVertices / nparts, "k_finish": 4 * single.ctVertices / nparts}
     # ... times the fp32 ops per lane-evaluation of that stage that the reference executes on
     # this input (its own op-box pruning included; the oracle's counters priced by
     # parsip_amd/costmodel.py, tests/golden/workload_ops.json); else the unpruned figure
@@ -342,7 +402,7 @@ def main():
         per_eval, per_src = wops[dom] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
     alg_ops = launch_evals[dom] * per_eval
     achieved = alg_ops / (kt[dom] * 1e-3) / 1e12
-    prof_ok = args.config == "C3" and grp.world == 1 and nstreams == 2 and args.jit == 1
+    prof_ok = args.config == "C3" and grp.world == 1 and (nparts, neng) == (1, 2) and args.jit == 1
     pmc, pmc_src = committed_profile("pmc")
     pe = profile_entry(pmc, dom, args.jit) if prof_ok else None
     tr, tr_src = committed_profile("traffic")
@@ -362,6 +422,12 @@ def main():
                     "averaged over the parts and repetitions of the timed engine; exact per-wave culling skips "
                     "part of those ops, so valu_issue (executed VALU instructions x 2 cycles per wave64 on "
                     "SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side utilisation"}
+    if dom in solo:
+        solo_evals = dict(launch_evals, k_mpu=512 * solo_fm / solo_n)[dom]
+        a_solo = solo_evals * per_eval / (solo[dom] * 1e-3) / 1e12
+        roof["isolated"] = {"kernel_ms": round(solo[dom], 4), "achieved": round(a_solo, 3),
+                            "frac": round(a_solo / VALU_PEAK_TFLOPS, 4),
+                            "note": "engine 0 alone on the device (no concurrent engine), same launches"}
     if pe and "SQ_INSTS_VALU" in pe:
         roof["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (kt[dom] * 1e-3 * 2.4e9 * 1024), 4)
         roof["valu_source"] = pmc_src
@@ -386,7 +452,10 @@ def main():
                                + (" split over the ranks (C4)" if full is not None else "")
                                + (", a grid per rank (frame = rank)" if scaling == "weak" and grp.world > 1 else ""),
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,
-                   "parallelism": f"{scaling}-{grp.world}gpu", "streams_per_gpu": nstreams,
+                   "parallelism": f"{scaling}-{grp.world}gpu", "engines_per_gpu": neng, "parts_per_engine": nparts,
+                   "streams_per_gpu": neng * nparts,
+                   "step": "one complete polygonization of the rank's MPU range (all four kernels); steps "
+                           "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
                    "exchange": exchange, "culling": not args.no_cull,
                    "kernels": ["interpreter", "jit-structure", "jit-baked"][args.jit] if jit_on or args.jit == 0
@@ -395,6 +464,7 @@ def main():
         "roofline": roof,
         "kernel_ms_per_launch": {k: round(v, 4) for k, v in kt.items()},
         "kernel_ms_per_launch_hipevent": {k: round(v, 4) for k, v in ev_ms.items()},
+        "kernel_ms_per_launch_isolated": {k: round(v, 4) for k, v in solo.items()},
         "mesh": {"vertices": info.ctVertices, "triangles": info.ctTriangles, "passed_s1": info.ctPassedPrecheck,
                  "surface_mpus": info.ctSurfaceMPUs, "field_mpus": info.ctFieldMPUs, "per_rank": counts},
         "hbm_gbs_algorithmic": round((mine.ctVertices * 36 + mine.ctTriangles * 12) / (ms_step * 1e-3) / 1e9, 2),
@@ -405,10 +475,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3)
     if grp.rank == 0:
         print(json.dumps(out), flush=True)
-    if comm:
-        comm.close()
-    if nstreams > 1:
-        eng.close()
+    for e in engines:
+        e.close()
     if grp.dist:
         grp.dist.destroy_process_group()
     poly.close()
