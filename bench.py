@@ -349,25 +349,29 @@ def main():
         if not ok:
             sys.exit(f"bench.py rank {grp.rank}: parts {counts} do not add up to the full grid {check['full']}")
 
-    # roofline pass: the same engines run concurrently as in the timed steps; per launch the
-    # device-clock span (first wave start -> last wave end) and the hipEvent bracket, so the
-    # per-launch averages are those of a rocprofv3 kernel trace of this command
+    # roofline pass: per-launch device-clock spans (first wave start -> last wave end) and
+    # hipEvent brackets in the regime of the timed steps: bursts of steps alternating between
+    # the engines, queued without host sync; the stamps keep each engine's last run, so the
+    # sample is the run of the engine that is NOT last in its burst (the other engine's next
+    # step still overlaps it, as in the steady state); the engine that goes last alternates
     for e in engines:
         e.set_option(gpu.OPT_KERNEL_TIMING, 1)
         e.set_option(gpu.OPT_STAMPS, 1 << 17)
     kt_sum, sp_sum, launches, fmpus = {}, {}, 0, 0
-    reps = max(3, min(args.steps, 20))
-    for _ in range(reps):
+    reps = max(4, min(args.steps, 20))
+    for rep in range(reps):
+        order = engines[rep % neng:] + engines[:rep % neng]
+        for k in range(3 * neng):
+            order[k % neng].polygonize()
         for e in engines:
-            e.polygonize()
-        for e in engines:
-            for ev, spn, fm in e.launch_times():
-                for k, v in ev.items():
-                    kt_sum[k] = kt_sum.get(k, 0.0) + v
-                for k, v in spn.items():
-                    sp_sum[k] = sp_sum.get(k, 0.0) + v
-                fmpus += fm
-                launches += 1
+            e.finish()
+        for ev, spn, fm in order[0].launch_times():
+            for k, v in ev.items():
+                kt_sum[k] = kt_sum.get(k, 0.0) + v
+            for k, v in spn.items():
+                sp_sum[k] = sp_sum.get(k, 0.0) + v
+            fmpus += fm
+            launches += 1
     # the same launches with the device to themselves (engine 0 alone): the per-kernel
     # figure without the other engine's kernels sharing the CUs
     solo_sum, solo_n, solo_fm = {}, 0, 0
@@ -413,15 +417,17 @@ def main():
             "traffic": round(te["traffic_bytes"]) if te and "traffic_bytes" in te else None,
             "traffic_source": tr_src if te else None,
             "kernel_ms": round(kt[dom], 4), "kernel_ms_source": "device-clock span per launch (first wave start to "
-            "last wave end, s_memrealtime), averaged over the parts and repetitions",
+            "last wave end, s_memrealtime), averaged over sampled launches in the timed steps' regime",
             "kernel_ms_hipevent": round(ev_ms[dom], 4), "launches_timed": launches,
             "lane_evals": round(launch_evals[dom]),
             "ops_per_eval": round(per_eval, 1), "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
             "note": "per launch: achieved = the lane-evaluations one launch performs (k_mpu: 512 x S2-evaluated "
-                    "MPUs of its part) x the reference's fp32 ops per evaluation / its hipEvent duration, "
-                    "averaged over the parts and repetitions of the timed engine; exact per-wave culling skips "
-                    "part of those ops, so valu_issue (executed VALU instructions x 2 cycles per wave64 on "
-                    "SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side utilisation"}
+                    "MPUs of its part) x the reference's fp32 ops per evaluation / its device-clock duration in "
+                    "the timed steps' regime (bursts alternating between the engines, the other engine's step "
+                    "overlapping); 'isolated' is the same launch with the device to itself. Exact per-wave "
+                    "culling skips part of those ops, so valu_issue (executed VALU instructions x 2 cycles per "
+                    "wave64 on SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side "
+                    "utilisation"}
     if dom in solo:
         solo_evals = dict(launch_evals, k_mpu=512 * solo_fm / solo_n)[dom]
         a_solo = solo_evals * per_eval / (solo[dom] * 1e-3) / 1e12

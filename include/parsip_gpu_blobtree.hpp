@@ -13,13 +13,15 @@
  *
  * The node classes named here are the reference's (PS::BLOBTREE, PS_BlobTree/include/):
  * CBlobNode (CBlobTree.h:29), CSkeletonPrimitive (CSkeletonPrimitive.h:24), the skeletons
- * CSkeletonPoint/Line/Ring/Disc/Cylinder/Cube/Triangle, and the operators CPcm,
- * CRicciBlend, CWarpTwist, CWarpTaper, CWarpBend, CWarpShear.
+ * CSkeletonPoint/Line/Ring/Disc/Cylinder/Cube/Triangle, CQuadricPoint, and the operators
+ * CPcm, CRicciBlend, CWarpTwist, CWarpTaper, CWarpBend, CWarpShear.  It also binds the
+ * compat mode (parsip_gpu_gui.hpp) as PS::CParsipOptimizedGpu.
  */
 #ifndef PARSIP_GPU_BLOBTREE_HPP
 #define PARSIP_GPU_BLOBTREE_HPP
 
 #include "parsip_gpu.hpp"
+#include "parsip_gpu_gui.hpp"
 
 struct ParsipBlobTreeApi {
     typedef PS::BLOBTREE::CBlobNode Node;
@@ -37,9 +39,18 @@ struct ParsipBlobTreeApi {
     typedef PS::BLOBTREE::CWarpTaper WarpTaper;
     typedef PS::BLOBTREE::CWarpBend WarpBend;
     typedef PS::BLOBTREE::CWarpShear WarpShear;
+    typedef PS::BLOBTREE::CQuadricPoint QuadricPoint;  // compat mode only (parsip_gpu_gui.hpp)
 };
 
 /* class SimdPoly (PS_HighPerformanceRender.h:15-33) on the device. */
 typedef psgpu::SimdPolyT<ParsipBlobTreeApi> SimdPoly;
+
+/* The GUI's own polygonizer (CParsipOptimized over a COMPACTBLOBTREE, CPolyParsipOptimized.h:
+ * 226-305) on the device: setup takes the BlobTree root (the compact conversion runs inside),
+ * the rest keeps the reference's names (run, countMPUs, stats*, drawMesh, exportMesh). */
+namespace PS {
+typedef psgpu::ParsipOptimizedT<ParsipBlobTreeApi> CParsipOptimizedGpu;
+typedef psgpu::CompactTreeT<ParsipBlobTreeApi> COMPACTBLOBTREEGpu;
+}  // namespace PS
 
 #endif /* PARSIP_GPU_BLOBTREE_HPP */

@@ -39,8 +39,10 @@ public:
     CMaterial material{};
     CAffineTransformation transform{};
     float res[4] = {0, 0, 0, 0};
+    int id = -1;
 
     int getNodeType() { return type; }
+    int getID() const { return id; }
     bool isOperator() { return type >= 14; }  // bntOpUnion and up (_constSettings.h:32)
     size_t countChildren() const { return kids.size(); }
     CBlobNode* getChild(size_t i) { return i < kids.size() ? kids[i] : nullptr; }
@@ -93,6 +95,15 @@ public:
     CSkeleton* skeleton = nullptr;
     ~CSkeletonPrimitive() override { delete skeleton; }
     CSkeleton* getSkeleton() { return skeleton; }
+};
+
+class CQuadricPoint : public CBlobNode {  // not a skeletal primitive (CompactBlobTree.cpp:369-377)
+public:
+    vec3f pos{};
+    float radius = 0.0f, scale = 0.0f;
+    vec3f getPosition() const { return pos; }
+    float getFieldRadius() const { return radius; }
+    float getFieldScale() const { return scale; }
 };
 
 class CPcm : public CBlobNode {

@@ -7,6 +7,12 @@
 //   run <tree.txt> <cellsize> <mesh.bin>
 //        the same, then SimdPoly::run on device 0 and SimdPoly::draw's per-MPU arrays
 //        (ctV, ctT, pos, nrm, col, U16 triangles per drawn MPU) into mesh.bin.
+//   gui-tree <tree.txt> <compact.bin>
+//        COMPACTBLOBTREE::convert (parsip_gpu_gui.hpp, CompactTreeT) of the same tree file:
+//        code, counts, then the prim / op / kid / matrix arrays.
+//   gui-run <tree.txt> <cellsize> <mesh.bin>
+//        PS::CParsipOptimizedGpu: setup over the root's octree + run on device 0, statistics
+//        and exportMesh (V, T, pos, nrm, rgba, mesh-wide triangle ids) into mesh.bin.
 //   soa <soa.bin> <cellsize> <polympus.bin>
 //        PS::SIMDPOLY::Polygonize on a PS::SIMDPOLY::PolyMPUs (24,000 MPUs, the reference's
 //        capacity); writes rc, ctMPUs and the MPUs.
@@ -26,16 +32,22 @@ using namespace PS::BLOBTREE;
 
 namespace {
 
-// One node per line, pre-order: type nKids lo3 hi3 diffuse3 identity back16 params12
+// One node per line, pre-order: type nKids lo3 hi3 diffuse3 identity back16 params12 alpha id
 // (params: a3 b3 c3 r h and res0..3 for operators, as the writer documents).
 CBlobNode* read_node(std::istream& in, std::vector<std::unique_ptr<CBlobNode>>& own) {
     int type, nk;
     in >> type >> nk;
     if (!in) return nullptr;
-    float v[3 + 3 + 3 + 1 + 16 + 12];
+    float v[3 + 3 + 3 + 1 + 16 + 12 + 2];
     for (float& f : v) in >> f;
     CBlobNode* n;
-    if (type >= 14) {
+    if (type == 10) {  // QuadricPoint: position, radius, scale in the skeleton slots
+        CQuadricPoint* q = new CQuadricPoint();
+        q->pos = vec3f{v[26], v[27], v[28]};
+        q->radius = v[35];
+        q->scale = v[36];
+        n = q;
+    } else if (type >= 14) {
         switch (type) {
         case 19: n = new CRicciBlend(); break;
         case 22: n = new CPcm(); break;
@@ -71,7 +83,8 @@ CBlobNode* read_node(std::istream& in, std::vector<std::unique_ptr<CBlobNode>>& 
     n->type = type;
     n->octree.lower = vec3f{v[0], v[1], v[2]};
     n->octree.upper = vec3f{v[3], v[4], v[5]};
-    n->material.diffused = vec4f{v[6], v[7], v[8], 1.0f};
+    n->material.diffused = vec4f{v[6], v[7], v[8], v[38]};
+    n->id = (int)v[39];
     n->transform.back.identity = v[9] != 0.0f;
     std::memcpy(n->transform.back.e, v + 10, 64);
     for (int k = 0; k < 4; ++k) n->res[k] = v[26 + k];
@@ -129,6 +142,48 @@ int main(int argc, char** argv) {
         poly.reset();
         std::fprintf(stderr, "destroyed\n");
         return dr == PSGPU_RET_SUCCESS ? 0 : 68;
+    }
+    if (mode == "gui-tree" || mode == "gui-run") {
+        std::ifstream in(argv[2]);
+        std::vector<std::unique_ptr<CBlobNode>> own;
+        CBlobNode* root = read_node(in, own);
+        if (!root) return 65;
+        if (mode == "gui-tree") {
+            PS::COMPACTBLOBTREEGpu tree;
+            const int code = tree.convert(root);
+            std::ofstream o(argv[3], std::ios::binary);
+            put(o, code);
+            const uint32_t n[4] = {(uint32_t)tree.prims.size(), (uint32_t)tree.ops.size(), (uint32_t)tree.kids.size(),
+                                   (uint32_t)tree.mtx.size()};
+            o.write(reinterpret_cast<const char*>(n), sizeof n);
+            o.write(reinterpret_cast<const char*>(tree.prims.data()), (std::streamsize)(n[0] * sizeof(PsGuiPrim)));
+            o.write(reinterpret_cast<const char*>(tree.ops.data()), (std::streamsize)(n[1] * sizeof(PsGuiOp)));
+            o.write(reinterpret_cast<const char*>(tree.kids.data()), (std::streamsize)(n[2] * 4));
+            o.write(reinterpret_cast<const char*>(tree.mtx.data()), (std::streamsize)(n[3] * sizeof(PsGuiMatrix)));
+            return 0;
+        }
+        if (argc < 5) return 64;
+        PS::CParsipOptimizedGpu p(0);
+        const int rs = p.setup(root, root->getOctree().lower, root->getOctree().upper, root->getID(),
+                               (float)std::atof(argv[3]));
+        const int rc = rs == PSGPU_RET_SUCCESS ? p.run() : rs;
+        std::printf("gui rc %d MPUs %zu V %u T %u evals %zu\n", rc, p.countMPUs(), p.info().ctVertices,
+                    p.info().ctTriangles, p.statsTotalFieldEvals());
+        if (rc != PSGPU_RET_SUCCESS) return 67;
+        std::vector<float> pos, nrm, col;
+        std::vector<uint32_t> tris;
+        const int re = p.exportMesh(pos, nrm, col, tris);
+        size_t drawnT = 0;
+        p.drawMesh([&](const float*, const float*, const float*, uint32_t, const uint32_t*, uint32_t nt) { drawnT += nt; });
+        if (drawnT != tris.size() / 3) return 69;
+        std::ofstream o(argv[4], std::ios::binary);
+        const uint32_t vt[2] = {(uint32_t)(pos.size() / 3), (uint32_t)(tris.size() / 3)};
+        o.write(reinterpret_cast<const char*>(vt), sizeof vt);
+        o.write(reinterpret_cast<const char*>(pos.data()), (std::streamsize)(pos.size() * 4));
+        o.write(reinterpret_cast<const char*>(nrm.data()), (std::streamsize)(nrm.size() * 4));
+        o.write(reinterpret_cast<const char*>(col.data()), (std::streamsize)(col.size() * 4));
+        o.write(reinterpret_cast<const char*>(tris.data()), (std::streamsize)(tris.size() * 4));
+        return re == PSGPU_RET_SUCCESS ? 0 : 68;
     }
     if (mode == "soa" && argc >= 5) {
         static PS::SIMDPOLY::SOABlobPrims prims;

@@ -73,8 +73,11 @@ def write_tree(root: bt.BlobNode, path: str) -> None:
             q[0:3], q[9] = p["position"], p["side"]
         elif t == B.PRIM_TRIANGLE:
             q[0:3], q[3:6], q[6:9] = p["corners"]
+        elif t == B.PRIM_QUADRICPOINT:
+            q[0:3], q[9], q[10] = p["position"], p["radius"], p["scale"]
         vals = [*_v3(lo), *_v3(hi), *_v3(n.material.diffused[:3]), 1.0 if back.is_identity() else 0.0,
-                *[float(x) for x in rows], *[float(np.float32(x)) for x in q]]
+                *[float(x) for x in rows], *[float(np.float32(x)) for x in q],
+                float(np.float32(n.material.diffused[3])), float(n.node_id)]
         lines.append(f"{int(t)} {len(n.children)} " + " ".join(repr(v) for v in vals))
         for c in n.children:
             rec(c)
@@ -208,3 +211,85 @@ def test_cpp_ps_simdpoly_polygonize(exe, tmp_path, oracle, name):
         v0, t0 = om.vertex_offsets[i], om.triangle_offsets[i]
         assert mpus["vPos"][i, :nv * 3].tobytes() == om.pos[v0:v0 + nv].tobytes()
         np.testing.assert_array_equal(mpus["triangles"][i, :nt * 3].reshape(-1, 3), om.tris[t0:t0 + nt])
+
+
+# ---- compat mode: COMPACTBLOBTREE::convert and CParsipOptimized in C++ (parsip_gpu_gui.hpp)
+def cpp_compact(exe, root, tmp_path):
+    tree, out = tmp_path / "tree.txt", tmp_path / "compact.bin"
+    write_tree(root, str(tree))
+    subprocess.run([exe, "gui-tree", str(tree), str(out)], check=True, timeout=60)
+    raw = open(out, "rb").read()
+    code = int(np.frombuffer(raw[:4], np.int32)[0])
+    nP, nO, nK, nM = (int(x) for x in np.frombuffer(raw[4:20], np.uint32))
+    at = 20
+    parts = []
+    for n, size in ((nP, 128), (nO, 80), (nK, 4), (nM, 64)):
+        parts.append(raw[at:at + n * size])
+        at += n * size
+    return code, parts
+
+
+def gui_all_types_tree():
+    from parsip_amd import gui
+
+    t = all_types_tree()
+    t.children.append(gui.QuadricPoint((0.2, 0.1, -0.3), 0.9, 1.3, material=bt.Material(diffused=(0.1, 0.2, 0.3, 0.5))))
+    t.children.append(bt.Op(B.OP_BLEND, bt.Point((0.0, 0.5, 0.0)), bt.Point((0.5, 0.5, 0.0)), bt.Cube((0.5, 0.0, 0.0), 0.1)))
+    for i, n in enumerate(_walk(t)):
+        n.node_id = 100 + i
+    return t
+
+
+def _walk(n):
+    yield n
+    for c in n.children:
+        yield from _walk(c)
+
+
+@pytest.mark.parametrize("which", ["train", "all_types"])
+def test_cpp_compact_tree_matches_python(exe, tmp_path, which):
+    """CompactTreeT<Api>::convert over the mock BlobTree gives the same COMPACTBLOBTREE arrays,
+    byte for byte, as parsip_amd/gui.py::compact_blobtree (n-ary operators kept)."""
+    from parsip_amd import gui, scene
+
+    root = (scene.load_scene(os.path.join(GOLDEN, "train_corrected.scene"))[0] if which == "train"
+            else gui_all_types_tree())
+    bt.compute_octrees(root)
+    code, parts = cpp_compact(exe, root, tmp_path)
+    pcode, tree = gui.compact_blobtree(root)
+    assert code == pcode == 0
+    for got, ref, what in zip(parts, (tree.prims, tree.ops, tree.kids, tree.mtx), ("prims", "ops", "kids", "mtx")):
+        assert got == ref.tobytes(), what
+
+
+def test_cpp_compact_tree_errors(exe, tmp_path):
+    bad = bt.Op(B.OP_UNION, bt.Point((0, 0, 0)), bt.Op(B.OP_GRADIENTBLEND, bt.Point((1, 0, 0)), bt.Point((0, 1, 0))))
+    code, _ = cpp_compact(exe, bad, tmp_path)
+    assert code == -5  # ERR_NODE_NOT_RECOGNIZED (CompactBlobTree.cpp:233-239)
+
+
+@pytest.mark.gpu
+def test_cpp_parsip_optimized_run_train(exe, tmp_path):
+    """PS::CParsipOptimizedGpu (compiled C++) setup + run + exportMesh + drawMesh on the device,
+    against the CPU restatement of CParsipOptimized (oracle/psgui.c): bit-exact."""
+    import psgui
+    from gui_util import bits
+    from parsip_amd import gui, scene
+
+    root = scene.load_scene(os.path.join(GOLDEN, "train_corrected.scene"))[0]
+    bt.compute_octrees(root)
+    tree, mesh = tmp_path / "tree.txt", tmp_path / "mesh.bin"
+    write_tree(root, str(tree))
+    r = subprocess.run([exe, "gui-run", str(tree), "0.2", str(mesh)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(mesh, "rb").read()
+    V, T = (int(x) for x in np.frombuffer(raw[:8], np.uint32))
+    _, ct = gui.compact_blobtree(root)
+    om = psgui.polygonize(ct, *ct.root_octree, 0.2, 0.5, threads=8)
+    assert (V, T) == (om.info.ctVertices, om.info.ctTriangles)
+    at = 8
+    for name, width in (("pos", 3), ("nrm", 3), ("col", 4)):
+        got = np.frombuffer(raw[at:at + V * width * 4], np.float32).reshape(-1, width)
+        at += V * width * 4
+        assert np.array_equal(bits(got), bits(getattr(om, name))), name
+    assert np.array_equal(np.frombuffer(raw[at:], np.uint32).reshape(-1, 3), om.tris)
