@@ -224,14 +224,28 @@ class Engine:
     def set_option(self, opt, val):
         self.obj.set_option(opt, val)
 
-    def launch_times(self):
-        """Per part of the last run: (hipEvent ms per kernel, device-clock spans, S2 MPUs)."""
+    def event_times(self):
+        """Per part of the last run: hipEvent ms per kernel (OPT_KERNEL_TIMING)."""
+        if self.p is not None:
+            self.p.finish()
+            return [self.p.kernel_times()]
+        self.obj.finish()
+        return [self.obj.kernel_times(i) for i in range(self.parts)]
+
+    def stamp_spans(self):
+        """Per part of the last run: (device-clock spans per kernel, S2-evaluated MPUs), from
+        the per-wave timeline (OPT_STAMPS)."""
         if self.p is not None:
             info = self.p.finish()
-            return [(self.p.kernel_times(), gpu.kernel_spans(self.p.stamps()), info.ctFieldMPUs)]
+            return [(gpu.kernel_spans(self.p.stamps()), info.ctFieldMPUs)]
         _, parts = self.obj.finish()
-        return [(self.obj.kernel_times(i), gpu.kernel_spans(self.obj.stamps(i)), parts[i].info.ctFieldMPUs)
-                for i in range(self.parts)]
+        return [(gpu.kernel_spans(self.obj.stamps(i)), parts[i].info.ctFieldMPUs) for i in range(self.parts)]
+
+    def spans(self):
+        """(launches, kernels) device-clock spans in ms recorded since OPT_SPANS, every part."""
+        if self.p is not None:
+            return self.p.spans()
+        return np.concatenate([self.obj.spans(i) for i in range(self.parts)])
 
     def close(self):
         if self.comm:
@@ -349,15 +363,30 @@ def main():
         if not ok:
             sys.exit(f"bench.py rank {grp.rank}: parts {counts} do not add up to the full grid {check['full']}")
 
-    # roofline pass: per-launch device-clock spans (first wave start -> last wave end) and
-    # hipEvent brackets in the regime of the timed steps: bursts of steps alternating between
-    # the engines, queued without host sync; the stamps keep each engine's last run, so the
-    # sample is the run of the engine that is NOT last in its burst (the other engine's next
-    # step still overlaps it, as in the steady state); the engine that goes last alternates
+    # roofline pass 1: the timed steps again, identically (K steps alternating between the
+    # engines, queued without host sync), with every launch recording its kernels' spans on
+    # the device clock (first wave start -> last wave end: one 64-bit atomic min / max per
+    # wave); per kernel, the average over all K launches
+    per_engine = (args.steps + neng - 1) // neng + 1
+    for e in engines:
+        e.set_option(gpu.OPT_SPANS, per_engine)
+    grp.barrier()
+    for k in range(args.steps):
+        engines[k % neng].polygonize()
+    for e in engines:
+        e.finish()
+    sp = np.concatenate([e.spans() for e in engines])
+    for e in engines:
+        e.set_option(gpu.OPT_SPANS, 0)
+    launches = len(sp)
+    kt = {k: float(sp[:, i].mean()) for i, k in enumerate(gpu.STAMP_KERNELS)}
+    fmpus = sum(e.local_info().ctFieldMPUs for e in engines) / neng * launches / nparts
+    # pass 2: hipEvent brackets around each kernel (they add the dispatch gap before each
+    # launch), in bursts alternating between the engines; the sample is the run of the engine
+    # that is not last in its burst
     for e in engines:
         e.set_option(gpu.OPT_KERNEL_TIMING, 1)
-        e.set_option(gpu.OPT_STAMPS, 1 << 17)
-    kt_sum, sp_sum, launches, fmpus = {}, {}, 0, 0
+    kt_sum, ev_n = {}, 0
     reps = max(4, min(args.steps, 20))
     for rep in range(reps):
         order = engines[rep % neng:] + engines[:rep % neng]
@@ -365,31 +394,28 @@ def main():
             order[k % neng].polygonize()
         for e in engines:
             e.finish()
-        for ev, spn, fm in order[0].launch_times():
+        for ev in order[0].event_times():
             for k, v in ev.items():
                 kt_sum[k] = kt_sum.get(k, 0.0) + v
-            for k, v in spn.items():
-                sp_sum[k] = sp_sum.get(k, 0.0) + v
-            fmpus += fm
-            launches += 1
+            ev_n += 1
+    for e in engines:
+        e.set_option(gpu.OPT_KERNEL_TIMING, 0)
+    ev_ms = {k: v / ev_n for k, v in kt_sum.items()}
+    for e in engines:
+        e.set_option(gpu.OPT_STAMPS, 1 << 17)
     # the same launches with the device to themselves (engine 0 alone): the per-kernel
     # figure without the other engine's kernels sharing the CUs
     solo_sum, solo_n, solo_fm = {}, 0, 0
     for _ in range(reps):
         engines[0].polygonize()
-        for _, spn, fm in engines[0].launch_times():
+        for spn, fm in engines[0].stamp_spans():
             for k, v in spn.items():
                 solo_sum[k] = solo_sum.get(k, 0.0) + v
             solo_fm += fm
             solo_n += 1
     for e in engines:
-        e.set_option(gpu.OPT_KERNEL_TIMING, 0)
         e.set_option(gpu.OPT_STAMPS, 0)
     solo = {k: v / solo_n for k, v in solo_sum.items()}
-    ev_ms = {k: v / launches for k, v in kt_sum.items()}  # hipEvent bracket per launch (ms)
-    # average launch duration: first wave start -> last wave end on the device clock
-    # (s_memrealtime stamps); the hipEvent brackets add the dispatch gap before each kernel
-    kt = {k: v / launches for k, v in sp_sum.items()} if len(sp_sum) == len(kt_sum) else ev_ms
     single = mine
     dom = max(kt, key=kt.get)
     # lane-evaluations one launch processes, on average (SURVEY.md §8(d) units) ...
@@ -417,14 +443,14 @@ def main():
             "traffic": round(te["traffic_bytes"]) if te and "traffic_bytes" in te else None,
             "traffic_source": tr_src if te else None,
             "kernel_ms": round(kt[dom], 4), "kernel_ms_source": "device-clock span per launch (first wave start to "
-            "last wave end, s_memrealtime), averaged over sampled launches in the timed steps' regime",
+            "last wave end, s_memrealtime), averaged over a replay of the K timed steps",
             "kernel_ms_hipevent": round(ev_ms[dom], 4), "launches_timed": launches,
             "lane_evals": round(launch_evals[dom]),
             "ops_per_eval": round(per_eval, 1), "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
             "note": "per launch: achieved = the lane-evaluations one launch performs (k_mpu: 512 x S2-evaluated "
-                    "MPUs of its part) x the reference's fp32 ops per evaluation / its device-clock duration in "
-                    "the timed steps' regime (bursts alternating between the engines, the other engine's step "
-                    "overlapping); 'isolated' is the same launch with the device to itself. Exact per-wave "
+                    "MPUs of its part) x the reference's fp32 ops per evaluation / its device-clock duration, "
+                    "averaged over an identical replay of the K timed steps (engines alternating, queued); "
+                    "'isolated' is the same launch with the device to itself. Exact per-wave "
                     "culling skips part of those ops, so valu_issue (executed VALU instructions x 2 cycles per "
                     "wave64 on SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side "
                     "utilisation"}

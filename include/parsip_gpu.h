@@ -226,6 +226,10 @@ int  psgpu_last_kernel_times(psgpu_ctx* ctx, float* ms, int maxKernels, const ch
  * mode 0 = consecutive points form the reference's 4-lane pruning groups,
  * mode 1 = every point alone (4 identical lanes), mode 2 = mode 1 + colour (n*3). */
 int  psgpu_field_values(psgpu_ctx* ctx, const float* xyz, uint32_t n, int mode, float* out, float* colOut);
+/* Kernel spans of the runs recorded since PSGPU_OPT_SPANS was set: *runs slots of
+ * 4 kernels x {start, end} (s_memrealtime, 100 MHz); out = NULL queries *runs. */
+int  psgpu_download_spans(psgpu_ctx* ctx, uint64_t* out, uint32_t* runs);
+
 /* Set a context option (see PSGPU_OPT_*). */
 int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_KERNEL_TIMING 1   /* 1: record hipEvents around every kernel */
@@ -244,6 +248,8 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        2 specialised with parameters baked in */
 #define PSGPU_OPT_STAMPS       12   /* > 0: record a per-wave timeline for up to this many waves
                                        per kernel (psgpu_download_stamps); 0: off (default) */
+#define PSGPU_OPT_SPANS        13   /* > 0: the next this-many runs record each kernel's span on the
+                                       device clock (first wave start, last wave end; 100 MHz) */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the
                                        specialised kernels on a host thread while the interpreter
                                        serves polygonizations (bit-identical output); 0: block */

@@ -620,12 +620,23 @@ __device__ __forceinline__ void phase_stamp(const Params& p, int ph, uint32_t bi
     const uint64_t t = stamp_now();
     if (lane_id() == 0) p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)w + ph] = t;
 }
+// A kernel's span in one run (PSGPU_OPT_SPANS): every wave folds its start / end into the
+// run's slot with one 64-bit atomic min / max each (lane 0), so the slot ends up holding the
+// first wave start and the last wave end on the device clock.
+__device__ __forceinline__ void span_end(const Params& p, int K, uint64_t t0) {
+    const uint64_t t1 = stamp_now();
+    if (lane_id() == 0) {
+        atomicMin(reinterpret_cast<unsigned long long*>(p.spans + 2 * K), (unsigned long long)t0);
+        atomicMax(reinterpret_cast<unsigned long long*>(p.spans + 2 * K + 1), (unsigned long long)t1);
+    }
+}
 #define PSGPU_STAMPED(K, ITEM, CALL)                                             \
     {                                                                             \
-        const uint64_t t0_ = p.stamps ? psgpu::stamp_now() : 0ull;                \
+        const uint64_t t0_ = (p.stamps || p.spans) ? psgpu::stamp_now() : 0ull;  \
         uint32_t item_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);     \
         CALL;                                                                     \
         if (p.stamps) psgpu::stamp_end(p, K, t0_, ITEM);                          \
+        if (p.spans) psgpu::span_end(p, K, t0_);                                  \
     }
 
 // ---------------------------------------------------------------------------

@@ -501,6 +501,7 @@ Params make_params(psgpu_ctx* c) {
     p.totals = c->totals;
     p.stamps = c->stamps;
     p.stampCap = c->stamps ? c->stampCap : 0u;
+    p.spans = (c->spans && c->spanNext < c->spanCap) ? c->spans + (size_t)c->spanNext * 2 * kNumStampKernels : nullptr;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     p.debug = (uint32_t)c->debug;
     return p;
@@ -556,6 +557,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         return PSGPU_RET_SUCCESS;
     }
     const Params p = make_params(c);
+    if (p.spans) c->spanNext++;
     c->runMpuBlocks = p.mpuBlocks;
     const uint32_t slot = c->parity;
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
@@ -858,7 +860,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     c->jitFut = JitFuture();
     c->jit.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
-                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps};
+                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hostCtr) (void)hipHostFree(c->hostCtr);
@@ -904,6 +906,24 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         jit_start(c);
     }
     else if (option == PSGPU_OPT_JIT_ASYNC) c->jitAsync = value != 0;
+    else if (option == PSGPU_OPT_SPANS && value >= 0 && value <= (1 << 20)) {
+        // the next `value` runs record their kernel spans, one slot each (then none)
+        if (c->pending) (void)hipStreamSynchronize(c->runStream);
+        if (c->spans) (void)hipFree(c->spans);
+        c->spans = nullptr;
+        c->spanCap = c->spanNext = 0;
+        drop_graphs(c);
+        if (value > 0) {
+            std::vector<uint64_t> init((size_t)value * 2 * kNumStampKernels);
+            for (size_t i = 0; i < init.size(); i += 2) {
+                init[i] = ~0ull;
+                init[i + 1] = 0ull;
+            }
+            PSGPU_CHECK(hipMalloc(&c->spans, init.size() * 8));
+            PSGPU_CHECK(hipMemcpy(c->spans, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+            c->spanCap = (uint32_t)value;
+        }
+    }
     else if (option == PSGPU_OPT_STAMPS && value >= 0 && value <= (1 << 24)) {
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
         if (c->stamps) (void)hipFree(c->stamps);
@@ -1051,6 +1071,17 @@ int psgpu_download_stamps(psgpu_ctx* c, uint64_t* out, uint32_t* capOut) {
     if (!c->stamps || !out) return c->stamps ? PSGPU_RET_SUCCESS : PSGPU_RET_PARAM_ERROR;
     PSGPU_CHECK(hipMemcpy(out, c->stamps, (size_t)kNumStampKernels * c->stampCap * 24 + (size_t)c->stampCap * 64,
                           hipMemcpyDeviceToHost));
+    return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_download_spans(psgpu_ctx* c, uint64_t* out, uint32_t* runs) {
+    if (!c || !runs) return PSGPU_RET_PARAM_ERROR;
+    *runs = c->spans ? c->spanNext : 0u;
+    if (!c->spans || !out || c->spanNext == 0) return PSGPU_RET_SUCCESS;
+    int rc = set_device(c);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (c->pending) PSGPU_CHECK(hipStreamSynchronize(c->runStream));
+    PSGPU_CHECK(hipMemcpy(out, c->spans, (size_t)c->spanNext * 2 * kNumStampKernels * 8, hipMemcpyDeviceToHost));
     return PSGPU_RET_SUCCESS;
 }
 

@@ -79,6 +79,8 @@ struct psgpu_ctx {
     uint32_t* totals = nullptr;         // 8 words of the last run's totals (k_finish), for RCCL
     uint64_t* stamps = nullptr;         // per-wave timeline (PSGPU_OPT_STAMPS), 4 x stampCap x 3 words
     uint32_t stampCap = 0;
+    uint64_t* spans = nullptr;          // per-run kernel spans (PSGPU_OPT_SPANS): spanCap x 4 x 2 words
+    uint32_t spanCap = 0, spanNext = 0;
     DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
     DevCounters* hostCtrDev = nullptr;  // its device address
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity

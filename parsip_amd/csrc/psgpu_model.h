@@ -231,6 +231,8 @@ struct Params {
                             // S2 MPUs, first overflow MPU, error (the parts' count exchange)
     uint64_t* stamps;       // per-wave timeline (PSGPU_OPT_STAMPS) or null: kNumStampKernels x
     uint32_t stampCap;      // stampCap records {start, end, item | hw id << 32} (s_memrealtime)
+    uint64_t* spans;        // PSGPU_OPT_SPANS: this run's slot, per kernel {first wave start, last
+                            // wave end} (atomic min / max of s_memrealtime), or null
     uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
     uint32_t debug;         // ablation switches for profiling (0 in production)
 };

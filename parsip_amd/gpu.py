@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_group_get_split", "psgpu_group_polygonize", "psgpu_group_finish", "psgpu_group_download_mesh",
     "psgpu_group_gather", "psgpu_group_export_polympus", "psgpu_group_polygonize_mpus",
     "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
-    "psgpu_comm_result", "psgpu_download_stamps", "psgpu_comm_exchange_group",
+    "psgpu_comm_result", "psgpu_download_stamps", "psgpu_comm_exchange_group", "psgpu_download_spans",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -74,6 +74,7 @@ OPT_GRAPH = 7
 OPT_BOUND = 10
 OPT_JIT_ASYNC = 11
 OPT_STAMPS = 12
+OPT_SPANS = 13
 STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
 BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3
@@ -118,6 +119,7 @@ def load(build_if_missing: bool = True):
         "psgpu_jit_compile": ([vp, vp, vp, i32, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
         "psgpu_mpu_costs": ([vp, vp], i32),
         "psgpu_download_stamps": ([vp, vp, ctypes.POINTER(u32)], i32),
+        "psgpu_download_spans": ([vp, vp, ctypes.POINTER(u32)], i32),
         "psgpu_split_costs": ([vp, u32, u32, u32, vp], i32),
         "psgpu_group_create": ([vp, i32, ctypes.POINTER(vp)], i32),
         "psgpu_group_destroy": ([vp], None),
@@ -339,6 +341,11 @@ class Polygonizer:
         of start, end (100 MHz ticks), item | hw id << 32, launched waves only."""
         return _stamps(self._L, self._ctx)
 
+    def spans(self) -> np.ndarray:
+        """(runs, kernels) device-clock kernel spans in ms of the runs recorded since
+        OPT_SPANS was set (kernels in STAMP_KERNELS order)."""
+        return _spans(self._L, self._ctx)
+
     def kernel_times(self) -> dict:
         """Per-kernel hipEvent times (ms) of the last finished run (OPT_KERNEL_TIMING)."""
         return _kernel_times(self._L, self._ctx)
@@ -469,6 +476,10 @@ class Group:
         """Per-kernel hipEvent times (ms) of part `part` in the last finished run."""
         return _kernel_times(self._L, ctypes.c_void_p(self.context_ptr(part)))
 
+    def spans(self, part: int) -> np.ndarray:
+        """Recorded kernel spans (OPT_SPANS) of part `part`: (runs, kernels) in ms."""
+        return _spans(self._L, ctypes.c_void_p(self.context_ptr(part)))
+
     def stamps(self, part: int) -> dict:
         """The per-wave timeline (OPT_STAMPS) of part `part` in the last finished run."""
         return _stamps(self._L, ctypes.c_void_p(self.context_ptr(part)))
@@ -484,6 +495,15 @@ def _stamps(L, ctx) -> dict:
     out = {k: buf[i][buf[i][:, 0] != 0] for i, k in enumerate(STAMP_KERNELS)}
     out["mpu_phases"] = raw[len(STAMP_KERNELS) * n * 3:].reshape(n, 8)
     return out
+
+
+def _spans(L, ctx) -> np.ndarray:
+    runs = ctypes.c_uint32()
+    _check(L.psgpu_download_spans(ctx, None, ctypes.byref(runs)), "psgpu_download_spans")
+    out = np.zeros((max(runs.value, 1), len(STAMP_KERNELS), 2), np.uint64)
+    _check(L.psgpu_download_spans(ctx, out.ctypes.data, ctypes.byref(runs)), "psgpu_download_spans")
+    out = out[:runs.value].astype(np.int64)
+    return (out[:, :, 1] - out[:, :, 0]) * 1e-5  # (runs, kernels) in ms (100 MHz ticks)
 
 
 def kernel_spans(stamps: dict) -> dict:
