@@ -6,16 +6,18 @@
 // :677-1092, baseColorOp :1124-1294, normal :433-450, ComputeRootNewtonRaphsonVEC4
 // :1581-1622).  The CPU restatement that checks it is oracle/psgui.c.
 //
-// One polygonization = 4 kernels on the context's stream (+ one count read-back):
+// One polygonization = 5 kernels on the context's stream (+ one count read-back):
 //   k_gui_classify  one wavefront per MPU: the octree test against every primitive (:164-183),
 //                   the 8^3 field cache (lane = (y, z), one 8-point walk along x), configs with
 //                   `f > iso`, per-MPU counts of new vertices / triangles / crossed cells;
 //   k_gui_scan      one block: the MPU offsets (exclusive scan in lattice order);
-//   k_gui_mesh      one wavefront per MPU with a surface: vertex ids in the reference's
+//   k_gui_edges     one wavefront per MPU with a surface: vertex ids in the reference's
 //                   creation order (the first cell in loop order that holds an edge, then
 //                   the candidate order of its table row: every cell around a crossing
-//                   edge lists it, so that cell is fixed by the edge's position), Newton
-//                   roots, normals and colours one vertex per lane, triangles per cell;
+//                   edge lists it, so that cell is fixed by the edge's position) as a
+//                   vertex task list, and the triangles per cell;
+//   k_gui_vertices  one mesh vertex per lane over the whole lattice: Newton root, normal,
+//                   colour (no MPU's vertex count sets a wave's length);
 //   k_gui_totals    one block: CParsipOptimized's statistics.
 // The tree walk is an interpreter over the compact arrays with a per-lane frame stack
 // (n-ary operators fold their kids as they arrive), bit-exact with the oracle:
@@ -73,6 +75,8 @@ struct Params {
     float* nrm;
     float* col;
     uint32_t* tris;
+    uint64_t* vtask;     // per mesh vertex: MPU | edge index << 32 (k_gui_edges -> k_gui_vertices)
+    uint32_t nV;         // mesh vertices of the run
     PsGuiInfo* totals;
 };
 
@@ -627,17 +631,17 @@ __global__ void __launch_bounds__(1024) k_gui_scan(Params p) {
     if (t == 0) p.offs[p.n] = carry;
 }
 
-__global__ void __launch_bounds__(64) k_gui_mesh(Params p) {
+// Per MPU with a surface (one wavefront): the reference's vertex creation order (edge ->
+// vertex id, as a vertex task list for k_gui_vertices) and the triangles in cell order,
+// table order (:312-317), with mesh-wide vertex ids.
+__global__ void __launch_bounds__(64) k_gui_edges(Params p) {
     __shared__ float fv[kCorners];
-    __shared__ uint16_t tbase[kCells + 1];
     __shared__ uint16_t edgeVid[kEdges];
-    __shared__ uint16_t vEdge[kEdges];
     const uint32_t m = blockIdx.x;
     const int lane = threadIdx.x;
     if (m >= p.n) return;
     const uint64_t cnt = p.counts[m];
-    const uint32_t V = (uint32_t)cnt, Tn = (uint32_t)(cnt >> 32);
-    if (V == 0u && Tn == 0u) return;
+    if (cnt == 0ull) return;
     const uint64_t off = p.offs[m];
     const uint32_t vOff = (uint32_t)off, tOff = (uint32_t)(off >> 32);
     for (int c = lane; c < kCorners; c += 64) fv[c] = p.fvc[(size_t)m * kCorners + c];
@@ -664,11 +668,12 @@ __global__ void __launch_bounds__(64) k_gui_mesh(Params p) {
         }
     }
     uint32_t vb = wave_excl_scan(nvL), tb = wave_excl_scan(ntL);
-    // vertex ids in creation order: edge -> id, id -> edge
+    uint32_t tbase[kCellsPerLane];
+    // vertex ids in creation order: edge -> id (LDS), id -> (MPU, edge) task
     for (int r = 0; r < kCellsPerLane; ++r) {
         const int cell = c0 + r;
-        if (cell >= c1) break;
-        tbase[cell] = (uint16_t)tb;
+        tbase[r] = tb;
+        if (cell >= c1) continue;
         const uint32_t cfg = cfgs[r];
         if (cfg == 0u) continue;
         tb += p.tables->ntri[cfg];
@@ -680,67 +685,12 @@ __global__ void __launch_bounds__(64) k_gui_mesh(Params p) {
             const int idx = edge_index(ci, cj, ck, (int)(e & 15u), &own);
             if (own && (e & 16u)) {
                 edgeVid[idx] = (uint16_t)vb;
-                vEdge[vb] = (uint16_t)idx;
+                p.vtask[(size_t)vOff + vb] = (uint64_t)m | ((uint64_t)idx << 32);
                 vb++;
             }
         }
     }
     __syncthreads();
-    // vertices: Newton root (:282-289), normal (:293), colour (:294), one per lane
-    float o[3];
-    mpu_origin(p, m, o);
-    const float iso = p.iso;
-    uint32_t evals = 0;
-    for (uint32_t v = lane; v < V; v += 64) {
-        int cc[2][3];
-        edge_corners(vEdge[v], cc);
-        V4 p1 = {o[0] + p.cs * (float)cc[0][0], o[1] + p.cs * (float)cc[0][1], o[2] + p.cs * (float)cc[0][2], 0.0f};
-        V4 p2 = {o[0] + p.cs * (float)cc[1][0], o[1] + p.cs * (float)cc[1][1], o[2] + p.cs * (float)cc[1][2], 0.0f};
-        const float fp1 = fv[corner_of(cc[0][0], cc[0][1], cc[0][2])];
-        const float fp2 = fv[corner_of(cc[1][0], cc[1][1], cc[1][2])];
-        V4 x = (fabsf(fp1 - iso) < fabsf(fp2 - iso)) ? p1 : p2;
-        const float inv = 1.0f / kFieldEps;
-        float outF = 0.0f;
-        int it;
-        for (it = 0; it < PSGUI_ITERATIONS; ++it) {
-            const float fp = field<false>(p.T, x.x, x.y, x.z, nullptr);
-            float gx = field<false>(p.T, x.x + kFieldEps, x.y + 0.0f, x.z + 0.0f, nullptr);
-            float gy = field<false>(p.T, x.x + 0.0f, x.y + kFieldEps, x.z + 0.0f, nullptr);
-            float gz = field<false>(p.T, x.x + 0.0f, x.y + 0.0f, x.z + kFieldEps, nullptr);
-            gx -= fp; gy -= fp; gz -= fp;
-            gx *= inv; gy *= inv; gz *= inv;
-            const float d = iso - fp;
-            const float gi = 1.0f / (gx * gx + gy * gy + gz * gz + fp * fp);
-            x.x = x.x + (d * gx) * gi;
-            x.y = x.y + (d * gy) * gi;
-            x.z = x.z + (d * gz) * gi;
-            x.w = x.w + (d * fp) * gi;
-            outF = field<false>(p.T, x.x, x.y, x.z, nullptr);
-            if (fabsf(outF - iso) < kFieldEps) break;
-        }
-        evals += (uint32_t)((it + 1) * 4) + 3u;  // the reference's count: (i + 1) * 4, + 3 (:282-292)
-        float c4[4];
-        (void)field<true>(p.T, x.x, x.y, x.z, c4);  // baseColor over the last walk's values
-        // normal (:433-450): forward differences, -1/delta, normalizeXYZ
-        const float ninv = -1.0f / kNormalDelta;
-        float nx = field<false>(p.T, x.x + kNormalDelta, x.y + 0.0f, x.z + 0.0f, nullptr);
-        float ny = field<false>(p.T, x.x + 0.0f, x.y + kNormalDelta, x.z + 0.0f, nullptr);
-        float nz = field<false>(p.T, x.x + 0.0f, x.y + 0.0f, x.z + kNormalDelta, nullptr);
-        nx -= outF; ny -= outF; nz -= outF;
-        nx *= ninv; ny *= ninv; nz *= ninv;
-        const float dn = sqrtf(nx * nx + ny * ny + nz * nz);
-        if (dn > 0) {
-            const float r = 1.0f / dn;
-            nx *= r; ny *= r; nz *= r;
-        } else {
-            nx = ny = nz = 1;
-        }
-        const size_t g = (size_t)vOff + v;
-        p.pos[3 * g] = x.x; p.pos[3 * g + 1] = x.y; p.pos[3 * g + 2] = x.z;
-        p.nrm[3 * g] = nx; p.nrm[3 * g + 1] = ny; p.nrm[3 * g + 2] = nz;
-        p.col[4 * g] = c4[0]; p.col[4 * g + 1] = c4[1]; p.col[4 * g + 2] = c4[2]; p.col[4 * g + 3] = c4[3];
-    }
-    // triangles in cell order, table order (:312-317), mesh-wide vertex ids
     for (int r = 0; r < kCellsPerLane; ++r) {
         const int cell = c0 + r;
         if (cell >= c1) break;
@@ -748,15 +698,73 @@ __global__ void __launch_bounds__(64) k_gui_mesh(Params p) {
         if (cfg == 0u) continue;
         const int ci = cell / (kC * kC), cj = (cell / kC) % kC, ck = cell % kC;
         const uint32_t nT = p.tables->ntri[cfg];
-        const size_t t0 = (size_t)tOff + tbase[cell];
+        const size_t t0 = (size_t)tOff + tbase[r];
         for (uint32_t q = 0; q < 3 * nT; ++q) {
             bool own;
             const int idx = edge_index(ci, cj, ck, (int)(p.tables->cand[cfg][q] & 15u), &own);
             p.tris[3 * t0 + q] = vOff + edgeVid[idx];
         }
     }
-    evals = wave_sum_u(evals);
-    if (lane == 0) p.stats[m].fieldEvals += evals;
+}
+
+// One mesh vertex per lane over the whole lattice: Newton root (:282-289), normal (:293),
+// colour (:294) of the vertex task's edge; field evaluations to its MPU's statistics.
+__global__ void __launch_bounds__(256) k_gui_vertices(Params p) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= p.nV) return;
+    const uint64_t task = p.vtask[g];
+    const uint32_t m = (uint32_t)task;
+    int cc[2][3];
+    edge_corners((int)(task >> 32), cc);
+    float o[3];
+    mpu_origin(p, m, o);
+    const float iso = p.iso;
+    V4 p1 = {o[0] + p.cs * (float)cc[0][0], o[1] + p.cs * (float)cc[0][1], o[2] + p.cs * (float)cc[0][2], 0.0f};
+    V4 p2 = {o[0] + p.cs * (float)cc[1][0], o[1] + p.cs * (float)cc[1][1], o[2] + p.cs * (float)cc[1][2], 0.0f};
+    const float* fv = p.fvc + (size_t)m * kCorners;
+    const float fp1 = fv[corner_of(cc[0][0], cc[0][1], cc[0][2])];
+    const float fp2 = fv[corner_of(cc[1][0], cc[1][1], cc[1][2])];
+    V4 x = (fabsf(fp1 - iso) < fabsf(fp2 - iso)) ? p1 : p2;
+    const float inv = 1.0f / kFieldEps;
+    float outF = 0.0f;
+    int it;
+    for (it = 0; it < PSGUI_ITERATIONS; ++it) {
+        const float fp = field<false>(p.T, x.x, x.y, x.z, nullptr);
+        float gx = field<false>(p.T, x.x + kFieldEps, x.y + 0.0f, x.z + 0.0f, nullptr);
+        float gy = field<false>(p.T, x.x + 0.0f, x.y + kFieldEps, x.z + 0.0f, nullptr);
+        float gz = field<false>(p.T, x.x + 0.0f, x.y + 0.0f, x.z + kFieldEps, nullptr);
+        gx -= fp; gy -= fp; gz -= fp;
+        gx *= inv; gy *= inv; gz *= inv;
+        const float d = iso - fp;
+        const float gi = 1.0f / (gx * gx + gy * gy + gz * gz + fp * fp);
+        x.x = x.x + (d * gx) * gi;
+        x.y = x.y + (d * gy) * gi;
+        x.z = x.z + (d * gz) * gi;
+        outF = field<false>(p.T, x.x, x.y, x.z, nullptr);
+        if (fabsf(outF - iso) < kFieldEps) break;
+    }
+    // the reference's count: (i + 1) * 4 for the root, + 3 for the normal (:282-292)
+    atomicAdd(&p.stats[m].fieldEvals, (uint32_t)((it + 1) * 4) + 3u);
+    float c4[4];
+    (void)field<true>(p.T, x.x, x.y, x.z, c4);  // baseColor over the last walk's values
+    // normal (:433-450): forward differences, -1/delta, normalizeXYZ
+    const float ninv = -1.0f / kNormalDelta;
+    float nx = field<false>(p.T, x.x + kNormalDelta, x.y + 0.0f, x.z + 0.0f, nullptr);
+    float ny = field<false>(p.T, x.x + 0.0f, x.y + kNormalDelta, x.z + 0.0f, nullptr);
+    float nz = field<false>(p.T, x.x + 0.0f, x.y + 0.0f, x.z + kNormalDelta, nullptr);
+    nx -= outF; ny -= outF; nz -= outF;
+    nx *= ninv; ny *= ninv; nz *= ninv;
+    const float dn = sqrtf(nx * nx + ny * ny + nz * nz);
+    if (dn > 0) {
+        const float r = 1.0f / dn;
+        nx *= r; ny *= r; nz *= r;
+    } else {
+        nx = ny = nz = 1;
+    }
+    p.pos[3 * (size_t)g] = x.x; p.pos[3 * (size_t)g + 1] = x.y; p.pos[3 * (size_t)g + 2] = x.z;
+    p.nrm[3 * (size_t)g] = nx; p.nrm[3 * (size_t)g + 1] = ny; p.nrm[3 * (size_t)g + 2] = nz;
+    p.col[4 * (size_t)g] = c4[0]; p.col[4 * (size_t)g + 1] = c4[1];
+    p.col[4 * (size_t)g + 2] = c4[2]; p.col[4 * (size_t)g + 3] = c4[3];
 }
 
 __global__ void __launch_bounds__(1024) k_gui_totals(Params p) {
@@ -824,6 +832,7 @@ struct psgpu_gui {
     PsGuiMpuStats* stats = nullptr;
     float *pos = nullptr, *nrm = nullptr, *col = nullptr;
     uint32_t* tris = nullptr;
+    uint64_t* vtask = nullptr;
     PsGuiInfo* dTotals = nullptr;
     PsGuiInfo* hTotals = nullptr;  // pinned
     PsGuiInfo lattice{};
@@ -957,7 +966,7 @@ void psgpu_gui_destroy(psgpu_gui* g) {
     (void)hipSetDevice(g->device);
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     void* bufs[] = {g->dP, g->dO, g->dK, g->dM, g->dTables, g->fvc, g->counts, g->offs, g->stats,
-                    g->pos, g->nrm, g->col, g->tris, g->dTotals};
+                    g->pos, g->nrm, g->col, g->tris, g->vtask, g->dTotals};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (g->hTotals) (void)hipHostFree(g->hTotals);
@@ -1049,15 +1058,16 @@ int psgpu_gui_polygonize(psgpu_gui* g, const float octLo[3], const float octHi[3
     GUI_CHECK(hipStreamSynchronize(g->stream));
     const size_t V = (uint32_t)tot, T = (uint32_t)(tot >> 32);
     if (V > g->capV || !g->pos) {
-        void* bufs[] = {g->pos, g->nrm, g->col};
+        void* bufs[] = {g->pos, g->nrm, g->col, g->vtask};
         for (void* b : bufs)
             if (b) (void)hipFree(b);
-        g->pos = nullptr; g->nrm = nullptr; g->col = nullptr;
+        g->pos = nullptr; g->nrm = nullptr; g->col = nullptr; g->vtask = nullptr;
         g->capV = 0;
         const size_t cv = std::max<size_t>(V + V / 8, 1024);
         GUI_CHECK(hipMalloc(&g->pos, cv * 12));
         GUI_CHECK(hipMalloc(&g->nrm, cv * 12));
         GUI_CHECK(hipMalloc(&g->col, cv * 16));
+        GUI_CHECK(hipMalloc(&g->vtask, cv * 8));
         g->capV = cv;
     }
     GUI_CHECK(grow(g->tris, g->capT, 3 * std::max<size_t>(T + T / 8, 1024)));
@@ -1065,8 +1075,14 @@ int psgpu_gui_polygonize(psgpu_gui* g, const float octLo[3], const float octHi[3
     p.nrm = g->nrm;
     p.col = g->col;
     p.tris = g->tris;
-    hipLaunchKernelGGL(psgui::k_gui_mesh, dim3(p.n), dim3(64), 0, g->stream, p);
+    p.vtask = g->vtask;
+    p.nV = (uint32_t)V;
+    hipLaunchKernelGGL(psgui::k_gui_edges, dim3(p.n), dim3(64), 0, g->stream, p);
     GUI_CHECK(hipGetLastError());
+    if (V > 0) {
+        hipLaunchKernelGGL(psgui::k_gui_vertices, dim3((unsigned)((V + 255) / 256)), dim3(256), 0, g->stream, p);
+        GUI_CHECK(hipGetLastError());
+    }
     hipLaunchKernelGGL(psgui::k_gui_totals, dim3(1), dim3(1024), 0, g->stream, p);
     GUI_CHECK(hipGetLastError());
     GUI_CHECK(hipMemcpyAsync(g->hTotals, g->dTotals, sizeof(PsGuiInfo), hipMemcpyDeviceToHost, g->stream));
