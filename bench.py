@@ -34,6 +34,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# HIP hands each process GPU_MAX_HW_QUEUES hardware queues (default 4) and maps streams onto
+# them round-robin: the engines (plus the planning context) need a queue each, or two
+# engines' kernels serialise on a shared queue.  Read at HIP init, so set before any HIP call.
+ENGINES_DEFAULT = 2
+HW_QUEUES_DEFAULT = 4
+for _i, _a in enumerate(sys.argv):  # --hw-queues N (GPU_MAX_HW_QUEUES; the box's default is 4)
+    if _a == "--hw-queues" and _i + 1 < len(sys.argv):
+        os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[_i + 1]
+os.environ.setdefault("GPU_MAX_HW_QUEUES", str(HW_QUEUES_DEFAULT))
 
 from parsip_amd import costmodel, gpu, synth  # noqa: E402  (no HIP call at import)
 
@@ -262,10 +271,12 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="N>1: strong (default: one grid split over the ranks) or weak (a grid per rank)")
-    ap.add_argument("--engines", type=int, default=2,
+    ap.add_argument("--engines", type=int, default=ENGINES_DEFAULT,
                     help="per device: this many engines (device contexts, each on its own HIP stream) take the "
                          "steps in turn; each step is a complete polygonization of the rank's range, queued "
                          "without host sync, so one run's kernel tails overlap the other's bulk")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; at most 32)")
     ap.add_argument("--parts", "--streams", type=int, default=1, dest="parts",
                     help="per engine: the range as this many cost-balanced parts on as many streams")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -432,7 +443,7 @@ def main():
         per_eval, per_src = wops[dom] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
     alg_ops = launch_evals[dom] * per_eval
     achieved = alg_ops / (kt[dom] * 1e-3) / 1e12
-    prof_ok = args.config == "C3" and grp.world == 1 and (nparts, neng) == (1, 2) and args.jit == 1
+    prof_ok = args.config == "C3" and grp.world == 1 and (nparts, neng) == (1, ENGINES_DEFAULT) and args.jit == 1
     pmc, pmc_src = committed_profile("pmc")
     pe = profile_entry(pmc, dom, args.jit) if prof_ok else None
     tr, tr_src = committed_profile("traffic")
@@ -485,7 +496,7 @@ def main():
                                + (", a grid per rank (frame = rank)" if scaling == "weak" and grp.world > 1 else ""),
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,
                    "parallelism": f"{scaling}-{grp.world}gpu", "engines_per_gpu": neng, "parts_per_engine": nparts,
-                   "streams_per_gpu": neng * nparts,
+                   "streams_per_gpu": neng * nparts, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                    "step": "one complete polygonization of the rank's MPU range (all four kernels); steps "
                            "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,

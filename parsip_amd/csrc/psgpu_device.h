@@ -620,14 +620,16 @@ __device__ __forceinline__ void phase_stamp(const Params& p, int ph, uint32_t bi
     const uint64_t t = stamp_now();
     if (lane_id() == 0) p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)w + ph] = t;
 }
-// A kernel's span in one run (PSGPU_OPT_SPANS): every wave folds its start / end into the
-// run's slot with one 64-bit atomic min / max each (lane 0), so the slot ends up holding the
-// first wave start and the last wave end on the device clock.
+// A kernel's span in one run (PSGPU_OPT_SPANS): every wave folds its start / end into one of
+// 64 {min start, max end} pairs of the run's slot (chosen by block, so no address sees more
+// than 1/64 of the waves' atomics); the host reduces the 64 pairs to the first wave start and
+// the last wave end on the device clock.
 __device__ __forceinline__ void span_end(const Params& p, int K, uint64_t t0) {
     const uint64_t t1 = stamp_now();
     if (lane_id() == 0) {
-        atomicMin(reinterpret_cast<unsigned long long*>(p.spans + 2 * K), (unsigned long long)t0);
-        atomicMax(reinterpret_cast<unsigned long long*>(p.spans + 2 * K + 1), (unsigned long long)t1);
+        uint64_t* s = p.spans + 2 * ((size_t)K * kSpanLanes + (blockIdx.x & (kSpanLanes - 1)));
+        atomicMin(reinterpret_cast<unsigned long long*>(s), (unsigned long long)t0);
+        atomicMax(reinterpret_cast<unsigned long long*>(s + 1), (unsigned long long)t1);
     }
 }
 #define PSGPU_STAMPED(K, ITEM, CALL)                                             \

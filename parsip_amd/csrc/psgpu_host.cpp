@@ -501,7 +501,8 @@ Params make_params(psgpu_ctx* c) {
     p.totals = c->totals;
     p.stamps = c->stamps;
     p.stampCap = c->stamps ? c->stampCap : 0u;
-    p.spans = (c->spans && c->spanNext < c->spanCap) ? c->spans + (size_t)c->spanNext * 2 * kNumStampKernels : nullptr;
+    p.spans = (c->spans && c->spanNext < c->spanCap)
+                  ? c->spans + (size_t)c->spanNext * 2 * kNumStampKernels * kSpanLanes : nullptr;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     p.debug = (uint32_t)c->debug;
     return p;
@@ -914,7 +915,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         c->spanCap = c->spanNext = 0;
         drop_graphs(c);
         if (value > 0) {
-            std::vector<uint64_t> init((size_t)value * 2 * kNumStampKernels);
+            std::vector<uint64_t> init((size_t)value * 2 * kNumStampKernels * kSpanLanes);
             for (size_t i = 0; i < init.size(); i += 2) {
                 init[i] = ~0ull;
                 init[i + 1] = 0ull;
@@ -1081,7 +1082,20 @@ int psgpu_download_spans(psgpu_ctx* c, uint64_t* out, uint32_t* runs) {
     int rc = set_device(c);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     if (c->pending) PSGPU_CHECK(hipStreamSynchronize(c->runStream));
-    PSGPU_CHECK(hipMemcpy(out, c->spans, (size_t)c->spanNext * 2 * kNumStampKernels * 8, hipMemcpyDeviceToHost));
+    const size_t per = (size_t)2 * kNumStampKernels * kSpanLanes;
+    std::vector<uint64_t> raw((size_t)c->spanNext * per);
+    PSGPU_CHECK(hipMemcpy(raw.data(), c->spans, raw.size() * 8, hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < c->spanNext; ++r)
+        for (int k = 0; k < kNumStampKernels; ++k) {
+            uint64_t lo = ~0ull, hi = 0ull;
+            for (int l = 0; l < kSpanLanes; ++l) {
+                const uint64_t* s = &raw[r * per + 2 * ((size_t)k * kSpanLanes + l)];
+                lo = std::min(lo, s[0]);
+                hi = std::max(hi, s[1]);
+            }
+            out[(size_t)r * 2 * kNumStampKernels + 2 * k] = lo;
+            out[(size_t)r * 2 * kNumStampKernels + 2 * k + 1] = hi;
+        }
     return PSGPU_RET_SUCCESS;
 }
 

@@ -185,6 +185,7 @@ struct DevCounters {
 constexpr int kMpuWaves = PSGPU_MPU_WAVES;
 constexpr int kMpusPerBlock = 4 / kMpuWaves;  // k_mpu blocks are 4 waves
 constexpr int kNumStampKernels = 4;  // k_precheck, k_mpu, k_vertex, k_finish
+constexpr int kSpanLanes = 64;       // {min start, max end} pairs per kernel per run (PSGPU_OPT_SPANS)
 
 // Kernel arguments of one polygonization (one struct, passed by value).
 struct Params {

@@ -1,0 +1,38 @@
+"""Strong-scaling rehearsal on one device: the ms/step of ONE rank's share of C3 (1/N of
+the cost-balanced split) as E engines take the steps in turn (queued, no host sync)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from parsip_amd import gpu, synth  # noqa: E402
+
+model, cs, N = synth.make_config("C3")
+plan = gpu.Polygonizer(0)
+plan.set_model(model)
+plan.run(cs)
+costs = plan.mpu_costs()
+for ranks in (1, 2, 4, 8):
+    b = gpu.split_costs(costs, ranks)
+    lo, hi = int(b[0]), int(b[1])
+    for neng in [int(x) for x in os.environ.get("ENGINES", "1,2,4").split(",")]:
+        ps = []
+        for _ in range(neng):
+            p = gpu.Polygonizer(0)
+            p.set_model(model)
+            p.run(cs, lo, hi)
+            ps.append(p)
+        K = 400
+        for k in range(20):
+            ps[k % neng].polygonize(cs, lo, hi)
+        for p in ps:
+            p.finish()
+        t0 = time.perf_counter()
+        for k in range(K):
+            ps[k % neng].polygonize(cs, lo, hi)
+        for p in ps:
+            p.finish()
+        dt = (time.perf_counter() - t0) / K * 1e3
+        print(f"rank share 1/{ranks} (MPUs {hi - lo}): {neng} engines {dt:.4f} ms/step", flush=True)
+        for p in ps:
+            p.close()

@@ -31,17 +31,22 @@ def main():
     ap.add_argument("--jit", type=int, default=1)
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--json")
+    ap.add_argument("--share", type=int, default=1, help="time the first 1/SHARE of the cost split (a rank's range)")
     a = ap.parse_args()
     model, cs, N = synth.make_config(a.config)
     p = gpu.Polygonizer(0)
     p.set_option(gpu.OPT_JIT, a.jit)
     p.set_model(model)
+    lo, hi = 0, None
+    if a.share > 1:
+        b = p.plan_split(cs, a.share)
+        lo, hi = int(b[0]), int(b[1])
     for _ in range(3):
-        p.run(cs)
+        p.run(cs, lo, hi)
     p.set_option(gpu.OPT_STAMPS, 1 << 17)
     report = {}
     for run in range(a.runs):
-        p.run(cs)
+        p.run(cs, lo, hi)
         S = p.stamps()
     prev_end = None
     first = min(int(S[k][:, 0].min()) for k in gpu.STAMP_KERNELS if len(S[k]))
