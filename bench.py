@@ -34,20 +34,30 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP hands each process GPU_MAX_HW_QUEUES hardware queues (default 4) and maps streams onto
-# them round-robin: the engines (plus the planning context) need a queue each, or two
-# engines' kernels serialise on a shared queue.  Read at HIP init, so set before any HIP call.
-ENGINES_DEFAULT = 2
-HW_QUEUES_DEFAULT = 4
-for _i, _a in enumerate(sys.argv):  # --hw-queues N (GPU_MAX_HW_QUEUES; the box's default is 4)
+# HIP hands each process GPU_MAX_HW_QUEUES hardware queues (the box's default is 4) and maps
+# streams onto them round-robin.  4 engines (one stream each) on queues of their own take the
+# most steps per second (tools/rt_fresh.sh: C3 0.068 ms/step at >= 6 queues vs 0.080 with 2
+# engines on 4; a 1/8 rank share 0.0165 vs 0.028); more than 4 concurrent streams is slower
+# again.  Read at HIP init, so set here, before any HIP call: --hw-queues N wins, else at
+# least HW_QUEUES_DEFAULT.
+ENGINES_DEFAULT = 4
+HW_QUEUES_DEFAULT = 8
+_hwq = None
+for _i, _a in enumerate(sys.argv):
     if _a == "--hw-queues" and _i + 1 < len(sys.argv):
-        os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[_i + 1]
-os.environ.setdefault("GPU_MAX_HW_QUEUES", str(HW_QUEUES_DEFAULT))
+        _hwq = sys.argv[_i + 1]
+if _hwq is None:
+    _hwq = str(max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4), HW_QUEUES_DEFAULT))
+os.environ["GPU_MAX_HW_QUEUES"] = _hwq
 
 from parsip_amd import costmodel, gpu, synth  # noqa: E402  (no HIP call at import)
 
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)": 256 CU x 4 SIMD-32 x 2.4 GHz x 64 (FMA)
 HBM_PEAK_GBS = 8000.0
+# reference-priced ops above the VALU peak: not a utilisation (frac is then null)
+FRAC_OVER_NOTE = (" (reference-priced ops / time exceeds the VALU peak: exact culling skips more of the tree "
+                  "than the reference's op-box pruning, so the reference's op count is not this launch's work; "
+                  "see valu_issue / the PMC profile for the hardware-side utilisation)")
 METRIC = "Mcells/sec polygonized, 256^3 grid 32-prim BlobTree, at 1/2/4/8 MI355X"
 
 
@@ -428,7 +438,9 @@ def main():
         e.set_option(gpu.OPT_STAMPS, 0)
     solo = {k: v / solo_n for k, v in solo_sum.items()}
     single = mine
-    dom = max(kt, key=kt.get)
+    # the dominant kernel: the longest with the device to itself (the replay spans of
+    # concurrent engines stretch whichever kernel overlaps the other engine's work)
+    dom = max(solo, key=solo.get) if solo else max(kt, key=kt.get)
     # lane-evaluations one launch processes, on average (SURVEY.md §8(d) units) ...
     launch_evals = {"k_precheck": 8 * single.ctMPUs / nparts, "k_mpu": 512 * fmpus / launches,
                     "k_vertex": 4 * single.ctVertices / nparts, "k_finish": 4 * single.ctVertices / nparts}
@@ -465,14 +477,24 @@ def main():
                     "culling skips part of those ops, so valu_issue (executed VALU instructions x 2 cycles per "
                     "wave64 on SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side "
                     "utilisation"}
+    roof["kernels_ms"] = {k: {"span": round(kt[k], 4), "hipevent": round(ev_ms.get(k, 0.0), 4),
+                              "isolated": round(solo.get(k, 0.0), 4)} for k in kt}
     if dom in solo:
         solo_evals = dict(launch_evals, k_mpu=512 * solo_fm / solo_n)[dom]
         a_solo = solo_evals * per_eval / (solo[dom] * 1e-3) / 1e12
         roof["isolated"] = {"kernel_ms": round(solo[dom], 4), "achieved": round(a_solo, 3),
                             "frac": round(a_solo / VALU_PEAK_TFLOPS, 4),
                             "note": "engine 0 alone on the device (no concurrent engine), same launches"}
+        if a_solo > VALU_PEAK_TFLOPS:
+            roof["isolated"]["frac"] = None
+            roof["isolated"]["note"] += FRAC_OVER_NOTE
+    if achieved > VALU_PEAK_TFLOPS:
+        roof["frac"] = None
+        roof["note"] += ";" + FRAC_OVER_NOTE
     if pe and "SQ_INSTS_VALU" in pe:
         roof["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (kt[dom] * 1e-3 * 2.4e9 * 1024), 4)
+        if dom in solo and "isolated" in roof:
+            roof["isolated"]["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (solo[dom] * 1e-3 * 2.4e9 * 1024), 4)
         roof["valu_source"] = pmc_src
     if te and "avg_us" in te:
         roof["rocprof_avg_us"] = te["avg_us"]

@@ -815,8 +815,10 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     const CubeTables& T = cube_tables();
     CubeTablesDev tabHost{};
     fill_device_tables(T, tabHost);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->dTables, sizeof(CubeTablesDev)) != hipSuccess ||
+    // the set-up copies run on the null stream BEFORE this context's stream exists: a process's
+    // first stream created ahead of the null stream's first use shares its hardware queue
+    // (tools/queue_probe.py: with 4 engines, the engine on that stream slowed every step ~25%)
+    if (hipMalloc(&c->dTables, sizeof(CubeTablesDev)) != hipSuccess ||
         hipMemcpy(c->dTables, &tabHost, sizeof(CubeTablesDev), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&c->dModel, sizeof(DevModel)) != hipSuccess ||
         hipMalloc(&c->ctr, 2 * sizeof(DevCounters)) != hipSuccess ||
@@ -824,7 +826,9 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
         hipMalloc(&c->scanStatus, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(c->scanStatus, 0, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&c->hostCtr, sizeof(DevCounters), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hostCtrDev), c->hostCtr, 0) != hipSuccess) {
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hostCtrDev), c->hostCtr, 0) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         psgpu_destroy(c);
         return PSGPU_RET_DEVICE_ERROR;
     }

@@ -12,7 +12,7 @@ plan = gpu.Polygonizer(0)
 plan.set_model(model)
 plan.run(cs)
 costs = plan.mpu_costs()
-for ranks in (1, 2, 4, 8):
+for ranks in [int(x) for x in os.environ.get("SHARES", "1,2,4,8").split(",")]:
     b = gpu.split_costs(costs, ranks)
     lo, hi = int(b[0]), int(b[1])
     for neng in [int(x) for x in os.environ.get("ENGINES", "1,2,4").split(",")]:
