@@ -34,8 +34,15 @@
 #ifndef PARSIP_GPU_H
 #define PARSIP_GPU_H
 
+#ifdef __HIPCC_RTC__  /* embedded in run-time compiled compat kernels: no system headers */
+typedef __SIZE_TYPE__ size_t;
+#ifndef offsetof
+#define offsetof(t, m) __builtin_offsetof(t, m)
+#endif
+#else
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -142,6 +142,24 @@ int  psgpu_gui_download(psgpu_gui* g, float* pos, float* nrm, float* col4, uint3
 /* COMPACTBLOBTREE::fieldvalue and baseColor at n points (probe; col4 may be NULL). */
 int  psgpu_gui_field_values(psgpu_gui* g, const float* xyz, uint32_t n, float* out, float* col4);
 
+/* Per-tree kernels.  set_tree starts compiling the tree's walk as straight-line code
+ * (hiprtc, on a host thread; parameters stay in device memory, so only a structural edit
+ * recompiles) while the interpreter kernels serve; polygonize swaps them in once loaded.
+ * Both are bit-identical.  PSGUI_OPT_JIT: 0 interpreter only, 1 swap in when ready
+ * (default; environment PSGUI_JIT overrides), 2 set_tree waits for the compile. */
+#define PSGUI_OPT_JIT           1
+#define PSGUI_JIT_NONE          0    /* interpreter (no compile requested)               */
+#define PSGUI_JIT_PENDING       1    /* compiling; the interpreter serves                */
+#define PSGUI_JIT_ACTIVE        2    /* the tree's kernels serve                         */
+#define PSGUI_JIT_FAILED        3    /* compile or load failed; the interpreter serves   */
+int  psgpu_gui_set_option(psgpu_gui* g, int option, int value);
+/* PSGUI_JIT_* of the current tree (wait != 0: block until its compile has finished). */
+int  psgpu_gui_jit_status(psgpu_gui* g, int wait);
+/* Compile a tree's kernels without a device (validation, cache warm-up): code-object
+ * bytes, or -1 with the compiler log in `log`; on success `log` holds the source. */
+long psgpu_gui_jit_compile(const PsGuiPrim* prims, uint32_t ctPrims, const PsGuiOp* ops, uint32_t ctOps,
+                           const uint32_t* kids, uint32_t ctKids, uint32_t ctMtx, char* log, size_t cap);
+
 #ifdef __cplusplus
 } /* extern "C" */
 static_assert(sizeof(PsGuiPrim) == 128, "PsGuiPrim size");

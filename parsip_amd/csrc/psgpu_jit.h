@@ -37,5 +37,8 @@ std::shared_ptr<JitKernels> jit_load(const JitCode& code, int device, std::strin
 long jit_compile_only(const DevModel& m, bool baked, std::string* err);
 // The generated HIP source (tests and debugging).
 std::string jit_source(const DevModel& m, bool baked);
+// Compat mode: compile a generated compact-tree source (psgpu_gui_jit.cpp) against the
+// embedded compat headers, with the same on-disk cache.  Blocking; no GPU needed.
+bool jit_compile_gui(const std::string& src, std::vector<char>& code, std::string* err);
 
 }  // namespace psgpu

@@ -216,7 +216,12 @@ _SIG = {
     "psgpu_gui_finish": (["vp", "pinfo"], "i32"),
     "psgpu_gui_download": (["vp", "vp", "vp", "vp", "vp", "vp", "vp"], "i32"),
     "psgpu_gui_field_values": (["vp", "vp", "u32", "vp", "vp"], "i32"),
+    "psgpu_gui_set_option": (["vp", "i32", "i32"], "i32"),
+    "psgpu_gui_jit_status": (["vp", "i32"], "i32"),
+    "psgpu_gui_jit_compile": (["vp", "u32", "vp", "u32", "vp", "u32", "u32", "vp", "size"], "long"),
 }
+OPT_JIT = 1
+JIT_NONE, JIT_PENDING, JIT_ACTIVE, JIT_FAILED = 0, 1, 2, 3
 EXPORTED_SYMBOLS = list(_SIG)
 
 
@@ -224,7 +229,8 @@ def _lib():
     L = gpu.load()
     if not getattr(L, "_gui_bound", False):
         T = {"i32": ctypes.c_int, "u32": ctypes.c_uint32, "f32": ctypes.c_float, "vp": ctypes.c_void_p,
-             "pvp": ctypes.POINTER(ctypes.c_void_p), "pinfo": ctypes.POINTER(PsGuiInfo), None: None}
+             "pvp": ctypes.POINTER(ctypes.c_void_p), "pinfo": ctypes.POINTER(PsGuiInfo), "size": ctypes.c_size_t,
+             "long": ctypes.c_long, None: None}
         for name, (args, res) in _SIG.items():
             fn = getattr(L, name)
             fn.argtypes = [T[a] for a in args]
@@ -233,13 +239,29 @@ def _lib():
     return L
 
 
-class ParsipOptimized:
-    """CParsipOptimized (CPolyParsipOptimized.h:226-305) on the MI355X library."""
+def jit_compile(tree: "CompactTree", cap: int = 1 << 22):
+    """Compile the tree's compat kernels without a device (hiprtc): (code-object bytes,
+    generated source); raises with the compiler log on failure."""
+    L = _lib()
+    buf = ctypes.create_string_buffer(cap)
+    p = tree.ptrs()
+    n = L.psgpu_gui_jit_compile(p[0], p[1], p[2], p[3], p[4], p[5], p[7], buf, cap)
+    if n < 0:
+        raise RuntimeError(f"psgpu_gui_jit_compile: {n}\n{buf.value.decode(errors='replace')}")
+    return n, buf.value.decode()
 
-    def __init__(self, device: int = 0):
+
+class ParsipOptimized:
+    """CParsipOptimized (CPolyParsipOptimized.h:226-305) on the MI355X library.  jit: 0 the
+    interpreter kernels only, 1 the tree's generated kernels once compiled (default), 2 wait
+    for them in set_tree."""
+
+    def __init__(self, device: int = 0, jit: int = None):
         self._L = _lib()
         self._g = ctypes.c_void_p()
         gpu._check(self._L.psgpu_gui_create(device, ctypes.byref(self._g)), "psgpu_gui_create")
+        if jit is not None:
+            gpu._check(self._L.psgpu_gui_set_option(self._g, OPT_JIT, int(jit)), "psgpu_gui_set_option")
         self._info = None
         self._tree = None
         self._setup = None
@@ -251,6 +273,13 @@ class ParsipOptimized:
             self._g = ctypes.c_void_p()
 
     __del__ = close
+
+    def jit_status(self, wait: bool = False) -> int:
+        """JIT_NONE / JIT_PENDING / JIT_ACTIVE / JIT_FAILED for the current tree."""
+        rc = self._L.psgpu_gui_jit_status(self._g, 1 if wait else 0)
+        if rc < 0:
+            gpu._check(rc, "psgpu_gui_jit_status")
+        return rc
 
     def set_tree(self, tree: CompactTree) -> None:
         rc = self._L.psgpu_gui_set_tree(self._g, *tree.ptrs())

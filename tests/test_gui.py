@@ -134,21 +134,39 @@ def test_reference_csv_consistency(train):
         assert abs(got[k] - ref[k]) / ref[k] < 0.02, (k, got[k], ref[k])
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_jit_source_compiles_on_host(seed):
+    """The generated compat kernels compile with hiprtc (no device needed)."""
+    code, tree = gui.compact_blobtree(random_tree(seed))
+    assert code == 0
+    n, src = gui.jit_compile(tree)
+    assert n > 10000 and "jit_gui_classify" in src and "prim_field_k" in src
+
+
 # ---------------------------------------------------------------- GPU --------
-@pytest.fixture(scope="module")
-def gui_ctx():
+# every GPU test runs on the interpreter kernels (jit 0) and on the tree's generated
+# kernels (jit 2: set_tree waits for them)
+@pytest.fixture(scope="module", params=[0, 2], ids=["interp", "jit"])
+def gui_ctx(request):
     from parsip_amd import gpu
 
     gpu.load()
     assert gpu.device_count() > 0, "no HIP device visible: GPU tests must run on an MI355X"
-    p = gui.ParsipOptimized(0)
+    p = gui.ParsipOptimized(0, jit=request.param)
+    p.jit_mode = request.param
     yield p
     p.close()
+
+
+def _expect_kernels(ctx):
+    want = gui.JIT_ACTIVE if ctx.jit_mode == 2 else gui.JIT_NONE
+    assert ctx.jit_status() == want
 
 
 def _both(ctx, tree, cs, iso=0.5, octree=None):
     lo, hi = octree if octree is not None else tree.root_octree
     ctx.setup(tree, (lo, hi), 0, cs, iso)
+    _expect_kernels(ctx)
     ctx.run()
     gm = ctx.exportMesh()
     om = psgui.polygonize(tree, lo, hi, cs, iso, threads=8)
@@ -186,6 +204,7 @@ def test_gpu_random_trees_bit_exact(gui_ctx, seed):
 def test_gpu_field_and_colour_probe(gui_ctx, train):
     _, tree = train
     gui_ctx.set_tree(tree)
+    _expect_kernels(gui_ctx)
     lo, hi = tree.root_octree
     xyz = np.random.default_rng(5).uniform(lo, hi, size=(20000, 3)).astype(np.float32)
     gf, gc = gui_ctx.field_values(xyz)

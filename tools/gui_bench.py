@@ -14,7 +14,7 @@ from parsip_amd import gui, scene  # noqa: E402
 
 
 def main():
-    sizes = [float(a) for a in sys.argv[1:]] or [0.13, 0.05]
+    sizes = [float(a) for a in sys.argv[1:] if not a.startswith("--")] or [0.13, 0.05]
     root = scene.load_scene(os.path.join(ROOT, "tests", "golden", "train_corrected.scene"))[0]
     code, tree = gui.compact_blobtree(root)
     p = gui.ParsipOptimized(0)
