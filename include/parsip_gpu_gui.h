@@ -148,6 +148,11 @@ int  psgpu_gui_field_values(psgpu_gui* g, const float* xyz, uint32_t n, float* o
  * Both are bit-identical.  PSGUI_OPT_JIT: 0 interpreter only, 1 swap in when ready
  * (default; environment PSGUI_JIT overrides), 2 set_tree waits for the compile. */
 #define PSGUI_OPT_JIT           1
+/* PSGUI_OPT_CULL (1 default; environment PSGUI_CULL overrides; takes effect at the next
+ * set_tree): skip a primitive, or a whole operator subtree, when no point of the wave lies
+ * in the world box outside which its field is exactly +0 (bounds through the node
+ * matrices, none below warps) -- results are bit-identical either way. */
+#define PSGUI_OPT_CULL          2
 #define PSGUI_JIT_NONE          0    /* interpreter (no compile requested)               */
 #define PSGUI_JIT_PENDING       1    /* compiling; the interpreter serves                */
 #define PSGUI_JIT_ACTIVE        2    /* the tree's kernels serve                         */
@@ -158,7 +163,13 @@ int  psgpu_gui_jit_status(psgpu_gui* g, int wait);
 /* Compile a tree's kernels without a device (validation, cache warm-up): code-object
  * bytes, or -1 with the compiler log in `log`; on success `log` holds the source. */
 long psgpu_gui_jit_compile(const PsGuiPrim* prims, uint32_t ctPrims, const PsGuiOp* ops, uint32_t ctOps,
-                           const uint32_t* kids, uint32_t ctKids, uint32_t ctMtx, char* log, size_t cap);
+                           const uint32_t* kids, uint32_t ctKids, const PsGuiMatrix* mtx, uint32_t ctMtx, int cull,
+                           char* log, size_t cap);
+/* The culling boxes set_tree derives (8 floats per primitive / operator: lo xyz, 0, hi xyz,
+ * 0; infinite where no exact bound exists, empty for Null); host only (tests, tools). */
+int  psgpu_gui_cull_boxes(const PsGuiPrim* prims, uint32_t ctPrims, const PsGuiOp* ops, uint32_t ctOps,
+                          const uint32_t* kids, uint32_t ctKids, const PsGuiMatrix* mtx, uint32_t ctMtx,
+                          float* primBoxes, float* opBoxes);
 
 #ifdef __cplusplus
 } /* extern "C" */

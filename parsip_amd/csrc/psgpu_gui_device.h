@@ -39,7 +39,17 @@ struct Tree {
     const uint32_t* __restrict__ K;
     const PsGuiMatrix* __restrict__ M;
     uint32_t nP, nO;
+    // exact culling (psgpu_gui_cull.cpp): per primitive / operator a world box (lo xyz, -,
+    // hi xyz, -) outside which its field / value is exactly +0; nullptr: no culling
+    const float* __restrict__ S;
+    const float* __restrict__ OS;
 };
+
+// Does any active lane's point lie in box b?  (A NaN coordinate counts as inside.)
+__device__ __forceinline__ bool box_live(const float* b, float x, float y, float z) {
+    const bool out = (x < b[0]) || (y < b[1]) || (z < b[2]) || (x > b[4]) || (y > b[5]) || (z > b[6]);
+    return __ballot(!out) != 0ull;
+}
 
 // Per (config, candidate position): edge | first-occurrence << 4 | valid << 5; per config
 // the triangle count.  Built on the host from the MC table.
@@ -469,7 +479,8 @@ __device__ float field(const Tree& T, float x, float y, float z, float* colOut) 
             if (k >> 16) {
                 init_frame(T, st[++sp], id, F.p);
             } else {
-                const float v = prim_field(T, id, F.p);
+                // a culled primitive's field is exactly +0 at every lane's point
+                const float v = (T.S == nullptr || box_live(T.S + 8 * id, x, y, z)) ? prim_field(T, id, F.p) : 0.0f;
                 fold<COLOR>(O, F, i, v, T.P[id].color);
             }
             continue;

@@ -218,9 +218,11 @@ _SIG = {
     "psgpu_gui_field_values": (["vp", "vp", "u32", "vp", "vp"], "i32"),
     "psgpu_gui_set_option": (["vp", "i32", "i32"], "i32"),
     "psgpu_gui_jit_status": (["vp", "i32"], "i32"),
-    "psgpu_gui_jit_compile": (["vp", "u32", "vp", "u32", "vp", "u32", "u32", "vp", "size"], "long"),
+    "psgpu_gui_jit_compile": (["vp", "u32", "vp", "u32", "vp", "u32", "vp", "u32", "i32", "vp", "size"], "long"),
+    "psgpu_gui_cull_boxes": (["vp", "u32", "vp", "u32", "vp", "u32", "vp", "u32", "vp", "vp"], "i32"),
 }
 OPT_JIT = 1
+OPT_CULL = 2
 JIT_NONE, JIT_PENDING, JIT_ACTIVE, JIT_FAILED = 0, 1, 2, 3
 EXPORTED_SYMBOLS = list(_SIG)
 
@@ -239,16 +241,28 @@ def _lib():
     return L
 
 
-def jit_compile(tree: "CompactTree", cap: int = 1 << 22):
+def jit_compile(tree: "CompactTree", cull: bool = True, cap: int = 1 << 22):
     """Compile the tree's compat kernels without a device (hiprtc): (code-object bytes,
     generated source); raises with the compiler log on failure."""
     L = _lib()
     buf = ctypes.create_string_buffer(cap)
     p = tree.ptrs()
-    n = L.psgpu_gui_jit_compile(p[0], p[1], p[2], p[3], p[4], p[5], p[7], buf, cap)
+    n = L.psgpu_gui_jit_compile(p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], 1 if cull else 0, buf, cap)
     if n < 0:
         raise RuntimeError(f"psgpu_gui_jit_compile: {n}\n{buf.value.decode(errors='replace')}")
     return n, buf.value.decode()
+
+
+def cull_boxes(tree: "CompactTree"):
+    """(prim boxes (nP, 2, 3), op boxes (nO, 2, 3)): world boxes outside which each node's
+    value is exactly +0 (host only)."""
+    L = _lib()
+    p = tree.ptrs()
+    pb = np.zeros((max(p[1], 1), 8), np.float32)
+    ob = np.zeros((max(p[3], 1), 8), np.float32)
+    gpu._check(L.psgpu_gui_cull_boxes(*p, pb.ctypes.data, ob.ctypes.data), "psgpu_gui_cull_boxes")
+    box = lambda a: np.stack([a[:, 0:3], a[:, 4:7]], axis=1)  # noqa: E731
+    return box(pb[:p[1]]), box(ob[:p[3]])
 
 
 class ParsipOptimized:
@@ -256,12 +270,14 @@ class ParsipOptimized:
     interpreter kernels only, 1 the tree's generated kernels once compiled (default), 2 wait
     for them in set_tree."""
 
-    def __init__(self, device: int = 0, jit: int = None):
+    def __init__(self, device: int = 0, jit: int = None, cull: bool = None):
         self._L = _lib()
         self._g = ctypes.c_void_p()
         gpu._check(self._L.psgpu_gui_create(device, ctypes.byref(self._g)), "psgpu_gui_create")
         if jit is not None:
             gpu._check(self._L.psgpu_gui_set_option(self._g, OPT_JIT, int(jit)), "psgpu_gui_set_option")
+        if cull is not None:
+            gpu._check(self._L.psgpu_gui_set_option(self._g, OPT_CULL, int(bool(cull))), "psgpu_gui_set_option")
         self._info = None
         self._tree = None
         self._setup = None

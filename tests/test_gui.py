@@ -134,6 +134,42 @@ def test_reference_csv_consistency(train):
         assert abs(got[k] - ref[k]) / ref[k] < 0.02, (k, got[k], ref[k])
 
 
+def _outside_shell(rng, box, n):
+    """n points in box widened by 25 % (at least 0.5) but outside box."""
+    lo, hi = box[0].astype(np.float64), box[1].astype(np.float64)
+    pad = np.maximum(0.25 * (hi - lo), 0.5)
+    pts = rng.uniform(lo - pad, hi + pad, size=(4 * n, 3))
+    out = ((pts < lo) | (pts > hi)).any(axis=1)
+    return pts[out][:n].astype(np.float32)
+
+
+def test_cull_boxes_are_conservative():
+    """Outside a node's culling box the field is exactly +0 (oracle): single primitives of
+    every type under random transforms and operators, and whole random trees outside the
+    root operator's box."""
+    rng = np.random.default_rng(11)
+    checked = 0
+    for seed in range(200):
+        code, tree = gui.compact_blobtree(random_tree(100 + seed, n_prims=1 + seed % 4))
+        assert code == 0
+        pb, ob = gui.cull_boxes(tree)
+        for box in list(pb) + [ob[0]]:
+            if not np.isfinite(box).all() or (box[0] > box[1]).any():
+                continue
+            pts = _outside_shell(rng, box, 400)
+            f, _ = psgui.field_values(tree, pts) if box is ob[0] else (None, None)
+            if box is ob[0]:
+                assert np.array_equal(bits(f), np.zeros(len(pts), np.uint32)), seed
+                checked += 1
+        # a single primitive: its own box bounds the tree's field
+        if len(pb) == 1 and np.isfinite(pb[0]).all() and (pb[0][0] <= pb[0][1]).all():
+            pts = _outside_shell(rng, pb[0], 400)
+            f, _ = psgui.field_values(tree, pts)
+            assert np.array_equal(bits(f), np.zeros(len(pts), np.uint32)), seed
+            checked += 1
+    assert checked > 40, checked
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 def test_jit_source_compiles_on_host(seed):
     """The generated compat kernels compile with hiprtc (no device needed)."""
@@ -145,15 +181,17 @@ def test_jit_source_compiles_on_host(seed):
 
 # ---------------------------------------------------------------- GPU --------
 # every GPU test runs on the interpreter kernels (jit 0) and on the tree's generated
-# kernels (jit 2: set_tree waits for them)
-@pytest.fixture(scope="module", params=[0, 2], ids=["interp", "jit"])
+# kernels (jit 2: set_tree waits for them), each with and without exact culling
+@pytest.fixture(scope="module", params=[(0, 1), (2, 1), (0, 0), (2, 0)],
+                ids=["interp", "jit", "interp-nocull", "jit-nocull"])
 def gui_ctx(request):
     from parsip_amd import gpu
 
     gpu.load()
     assert gpu.device_count() > 0, "no HIP device visible: GPU tests must run on an MI355X"
-    p = gui.ParsipOptimized(0, jit=request.param)
-    p.jit_mode = request.param
+    jit, cull = request.param
+    p = gui.ParsipOptimized(0, jit=jit, cull=cull)
+    p.jit_mode = jit
     yield p
     p.close()
 
