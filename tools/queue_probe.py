@@ -31,8 +31,13 @@ if os.environ.get("TORCH", "0") == "1":
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
     dist.init_process_group("gloo", rank=0, world_size=1)
+VB, FB = int(os.environ.get("VB", "0")), int(os.environ.get("FB", "0"))  # persistent grids (blocks per CU)
 for _ in range(E):
     p = gpu.Polygonizer(0)
+    if VB:
+        p.set_option(gpu.OPT_VERTEX_BLOCKS_PER_CU, VB)
+    if FB:
+        p.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, FB)
     p.set_model(model)
     if os.environ.get("PRERUN", "0") == "1":
         p.run(cs, 0, n)
@@ -53,4 +58,4 @@ for rep in range(3):
         p.finish()
     dt = (time.perf_counter() - t0) / K * 1e3
     print(f"E={E} EXTRA={os.environ.get('EXTRA', '0')} PRERUN={os.environ.get('PRERUN', '0')} "
-          f"TORCH={os.environ.get('TORCH', '0')} q={os.environ.get('GPU_MAX_HW_QUEUES')}: {dt:.4f} ms/step", flush=True)
+          f"TORCH={os.environ.get('TORCH', '0')} q={os.environ.get('GPU_MAX_HW_QUEUES')} VB={VB} FB={FB}: {dt:.4f} ms/step", flush=True)
