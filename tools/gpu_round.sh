@@ -10,9 +10,10 @@ set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 if [ "$2" = "--collect" ]; then
-  for f in kernel_stats.csv traffic.json pmc.json bench.json bench_c5.json; do
+  for f in kernel_stats.csv traffic.json pmc.json bench.json bench_c5.json gui_bench.jsonl gui_kernel_stats.csv; do
     src=$OUT/$f; [ $f = kernel_stats.csv ] && src=$OUT/kt/run_kernel_stats.csv
     [ $f = pmc.json ] && src=$OUT/pmc/pmc.json
+    [ $f = gui_kernel_stats.csv ] && src=$OUT/guikt/run_kernel_stats.csv
     [ -f $src ] && cp $src profiles/${TAG}_$f
   done
   exit 0
@@ -39,3 +40,8 @@ cp $OUT/bench.json profiles/${TAG}_bench.json
 cat $OUT/bench.json
 timeout -k 10 300 python3 bench.py --config C5 --no-cpu --steps 50 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -20 $OUT/bench_c5.err; exit 1; }
 cat $OUT/bench_c5.json
+# compat mode (the GUI path): the train scene at three cell sizes, generated kernels, and its
+# kernel trace at cellsize 0.03
+PSGUI_JIT=2 timeout -k 10 300 python3 tools/gui_bench.py 0.13 0.05 0.03 > $OUT/gui_bench.jsonl 2> $OUT/gui_bench.err || { tail -20 $OUT/gui_bench.err; exit 1; }
+cat $OUT/gui_bench.jsonl
+PSGUI_JIT=2 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/guikt -o run -- python3 tools/gui_bench.py 0.03 --no-cpu > $OUT/guikt.log 2>&1 || { tail -20 $OUT/guikt.log; exit 1; }
