@@ -91,6 +91,23 @@ def test_random_trees(gpu_poly, oracle, seed):
     assert_mesh_matches(gm, gs, om)
 
 
+def test_max_size_tree(gpu_poly, oracle):
+    """The SoA limits: 128 primitives (cull masks' high word, 8-bit child ids) and 127 ops,
+    every primitive type and op, matrices; interpreter kernels (the generated kernels of a
+    128-primitive tree take ~2 minutes of hiprtc)."""
+    ops = [NodeType.BLEND, NodeType.UNION, NodeType.INTERSECT, NodeType.DIF, NodeType.SMOOTHDIF,
+           NodeType.RICCIBLEND]
+    types = [NodeType.POINT, NodeType.LINE, NodeType.CYLINDER, NodeType.CUBE, NodeType.DISC, NodeType.RING,
+             NodeType.TRIANGLE]
+    model = synth.random_model(99, n_prims=128, types=types, op_types=ops, matrices=True)
+    assert int(model.prims["ctPrims"][0]) == 128 and int(model.ops["ctOps"][0]) == 127
+    cs = float(np.float32(4.0 / 40))
+    for cull in (1, 0):
+        gm, gs, om = run_both(gpu_poly, oracle, model, cs, cull=cull, jit=0)
+        assert len(gm.pos) > 10000
+        assert_mesh_matches(gm, gs, om)
+
+
 def test_disc_ring_triangle_null(gpu_poly, oracle):
     """Every primitive switch case incl. rsqrt users and the no-case default."""
     types = [NodeType.DISC, NodeType.RING, NodeType.POINT, NodeType.TRIANGLE, NodeType.CUBE]
