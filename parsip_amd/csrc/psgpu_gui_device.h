@@ -43,12 +43,40 @@ struct Tree {
     // hi xyz, -) outside which its field / value is exactly +0; nullptr: no culling
     const float* __restrict__ S;
     const float* __restrict__ OS;
+    // masked != 0: per-wave live bits (primitives / operators 0-127) replace the per-point
+    // box tests -- set by a kernel whose wave's points all lie in a known box
+    uint64_t pm0, pm1, om0, om1;
+    uint32_t masked;
 };
 
 // Does any active lane's point lie in box b?  (A NaN coordinate counts as inside.)
 __device__ __forceinline__ bool box_live(const float* b, float x, float y, float z) {
     const bool out = (x < b[0]) || (y < b[1]) || (z < b[2]) || (x > b[4]) || (y > b[5]) || (z > b[6]);
     return __ballot(!out) != 0ull;
+}
+__device__ __forceinline__ bool bit_of(uint64_t w0, uint64_t w1, uint32_t i) {
+    return ((i < 64 ? (w0 >> i) : (w1 >> (i - 64))) & 1ull) != 0ull;
+}
+// Primitive / operator i reached by a point of the wave (T.S / T.OS non-null)
+__device__ __forceinline__ bool prim_live(const Tree& T, uint32_t i, float x, float y, float z) {
+    return T.masked ? bit_of(T.pm0, T.pm1, i) : box_live(T.S + 8 * i, x, y, z);
+}
+__device__ __forceinline__ bool op_live(const Tree& T, uint32_t i, float x, float y, float z) {
+    return T.masked ? bit_of(T.om0, T.om1, i) : box_live(T.OS + 8 * i, x, y, z);
+}
+// Live bits of every node whose box meets [lo, hi] (one wave, all lanes active): a node
+// whose box misses it is +0 at every point inside it.
+__device__ __forceinline__ void mask_for_box(Tree& T, float lx, float ly, float lz, float hx, float hy, float hz) {
+    if (!T.S || T.nP > 128u || T.nO > 128u) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    auto meets = [&](const float* b) {
+        return !(hx < b[0] || hy < b[1] || hz < b[2] || lx > b[4] || ly > b[5] || lz > b[6]);
+    };
+    T.pm0 = __ballot(lane < T.nP && meets(T.S + 8 * lane));
+    T.pm1 = __ballot(lane + 64u < T.nP && meets(T.S + 8 * (lane + 64u)));
+    T.om0 = __ballot(lane < T.nO && meets(T.OS + 8 * lane));
+    T.om1 = __ballot(lane + 64u < T.nO && meets(T.OS + 8 * (lane + 64u)));
+    T.masked = 1u;
 }
 
 // Per (config, candidate position): edge | first-occurrence << 4 | valid << 5; per config
@@ -480,7 +508,7 @@ __device__ float field(const Tree& T, float x, float y, float z, float* colOut) 
                 init_frame(T, st[++sp], id, F.p);
             } else {
                 // a culled primitive's field is exactly +0 at every lane's point
-                const float v = (T.S == nullptr || box_live(T.S + 8 * id, x, y, z)) ? prim_field(T, id, F.p) : 0.0f;
+                const float v = (T.S == nullptr || prim_live(T, id, x, y, z)) ? prim_field(T, id, F.p) : 0.0f;
                 fold<COLOR>(O, F, i, v, T.P[id].color);
             }
             continue;
@@ -506,6 +534,22 @@ struct InterpField {
         return field<COLOR>(T, x, y, z, colOut);
     }
 };
+
+__device__ __forceinline__ float wave_min_f(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+// Live masks from the AABB of the 64 lanes' points (all lanes active); a NaN coordinate
+// anywhere keeps the per-point box tests.
+__device__ __forceinline__ void wave_mask(Tree& T, float px, float py, float pz) {
+    if (!T.S || T.nP > 128u || T.nO > 128u) return;
+    if (__ballot(!(px == px) || !(py == py) || !(pz == pz)) != 0ull) return;
+    mask_for_box(T, wave_min_f(px), wave_min_f(py), wave_min_f(pz), wave_max_f(px), wave_max_f(py), wave_max_f(pz));
+}
 
 __device__ __forceinline__ float wave_sum_f(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -613,13 +657,18 @@ __device__ __forceinline__ void classify_body(const Params& p, float* fv) {
         }
         return;
     }
-    // the field cache: corner (i, j, k) at org + cs * (i, j, k) (:193-238)
+    // the field cache: corner (i, j, k) at org + cs * (i, j, k) (:193-238); the x-slice i's
+    // corners lie in {x} x [org.y, org.y + cs * 7] x [org.z, org.z + cs * 7] (the lanes' own
+    // expressions at the extreme indices): one live mask per slice
+    const float yHi = o[1] + p.cs * 7.0f, zHi = o[2] + p.cs * 7.0f;
     const int j = lane >> 3, k = lane & 7;
     const float y = o[1] + p.cs * (float)j, z = o[2] + p.cs * (float)k;
 #pragma unroll 1
     for (int i = 0; i < kG; ++i) {
         const float x = o[0] + p.cs * (float)i;
-        const float f = EV::template eval<false>(p.T, x, y, z, nullptr);
+        Tree T = p.T;
+        mask_for_box(T, x, o[1], o[2], x, yHi, zHi);
+        const float f = EV::template eval<false>(T, x, y, z, nullptr);
         fv[corner_of(i, j, k)] = f;
         p.fvc[(size_t)m * kCorners + corner_of(i, j, k)] = f;
     }
@@ -661,41 +710,56 @@ __device__ __forceinline__ void vertices_body(const Params& p) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t g = t >> 2;
     const int q = (int)(t & 3u);
-    if (g >= p.nV) return;  // whole quads: the four lanes share g
+    const bool valid = g < p.nV;  // whole quads: the four lanes share g
     const int base = (int)(threadIdx.x & 63u) & ~3;
-    const uint64_t task = p.vtask[g];
-    const uint32_t m = (uint32_t)task;
-    int cc[2][3];
-    edge_corners((int)(task >> 32), cc);
-    float o[3];
-    mpu_origin(p, m, o);
+    uint32_t m = 0;
+    V4 x = {0.0f, 0.0f, 0.0f, 0.0f};
     const float iso = p.iso;
-    V4 p1 = {o[0] + p.cs * (float)cc[0][0], o[1] + p.cs * (float)cc[0][1], o[2] + p.cs * (float)cc[0][2], 0.0f};
-    V4 p2 = {o[0] + p.cs * (float)cc[1][0], o[1] + p.cs * (float)cc[1][1], o[2] + p.cs * (float)cc[1][2], 0.0f};
-    const float* fv = p.fvc + (size_t)m * kCorners;
-    const float fp1 = fv[corner_of(cc[0][0], cc[0][1], cc[0][2])];
-    const float fp2 = fv[corner_of(cc[1][0], cc[1][1], cc[1][2])];
-    V4 x = (fabsf(fp1 - iso) < fabsf(fp2 - iso)) ? p1 : p2;
+    if (valid) {
+        const uint64_t task = p.vtask[g];
+        m = (uint32_t)task;
+        int cc[2][3];
+        edge_corners((int)(task >> 32), cc);
+        float o[3];
+        mpu_origin(p, m, o);
+        V4 p1 = {o[0] + p.cs * (float)cc[0][0], o[1] + p.cs * (float)cc[0][1], o[2] + p.cs * (float)cc[0][2], 0.0f};
+        V4 p2 = {o[0] + p.cs * (float)cc[1][0], o[1] + p.cs * (float)cc[1][1], o[2] + p.cs * (float)cc[1][2], 0.0f};
+        const float* fv = p.fvc + (size_t)m * kCorners;
+        const float fp1 = fv[corner_of(cc[0][0], cc[0][1], cc[0][2])];
+        const float fp2 = fv[corner_of(cc[1][0], cc[1][1], cc[1][2])];
+        x = (fabsf(fp1 - iso) < fabsf(fp2 - iso)) ? p1 : p2;
+    }
     const float inv = 1.0f / kFieldEps;
     float outF = 0.0f;
     int itFinal = PSGUI_ITERATIONS;
+    bool done = !valid;
+    // every lane stays in the loop until the whole wave is done (finished quads walk their
+    // last point again and ignore it), so each round's culling masks come from all 64 lanes
     for (int r = 0;; ++r) {
+        if (__ballot(!done) == 0ull) break;
         float px = x.x, py = x.y, pz = x.z;
         if (q < 3) {  // x + eps * e_q, the reference's `+ 0.0f` kept
             px = x.x + (q == 0 ? kFieldEps : 0.0f);
             py = x.y + (q == 1 ? kFieldEps : 0.0f);
             pz = x.z + (q == 2 ? kFieldEps : 0.0f);
         }
-        const float f = EV::template eval_call<false>(p.T, px, py, pz, nullptr);
+        Tree T = p.T;
+        wave_mask(T, px, py, pz);
+        const float f = EV::template eval_call<false>(T, px, py, pz, nullptr);
         const float fx = __shfl(f, base + 0), fy = __shfl(f, base + 1), fz = __shfl(f, base + 2);
         const float fc = __shfl(f, base + 3);
+        if (done) continue;
         if (r >= 1) {  // fc = f(x) = the step of iteration r - 1's outF
             outF = fc;
             if (fabsf(outF - iso) < kFieldEps) {
                 itFinal = r - 1;
-                break;
+                done = true;
+                continue;
             }
-            if (r - 1 == PSGUI_ITERATIONS - 1) break;  // the loop ran out: i == DEFAULT_ITERATIONS
+            if (r - 1 == PSGUI_ITERATIONS - 1) {  // the loop ran out: i == DEFAULT_ITERATIONS
+                done = true;
+                continue;
+            }
         }
         const float fp = fc;
         float gx = fx, gy = fy, gz = fz;
@@ -715,11 +779,13 @@ __device__ __forceinline__ void vertices_body(const Params& p) {
         pz = x.z + (q == 2 ? kNormalDelta : 0.0f);
     }
     float c4[4];
-    const float f = EV::template eval_call<true>(p.T, px, py, pz, c4);
+    Tree T = p.T;
+    wave_mask(T, px, py, pz);
+    const float f = EV::template eval_call<true>(T, px, py, pz, c4);
     float nx = __shfl(f, base + 0), ny = __shfl(f, base + 1), nz = __shfl(f, base + 2);
     const float col0 = __shfl(c4[0], base + 3), col1 = __shfl(c4[1], base + 3);
     const float col2 = __shfl(c4[2], base + 3), col3 = __shfl(c4[3], base + 3);
-    if (q != 0) return;
+    if (q != 0 || !valid) return;
     atomicAdd(&p.stats[m].fieldEvals, (uint32_t)((itFinal + 1) * 4) + 3u);
     const float ninv = -1.0f / kNormalDelta;
     nx -= outF; ny -= outF; nz -= outF;
