@@ -38,7 +38,7 @@ cat $OUT/traffic.json
 timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cp $OUT/bench.json profiles/${TAG}_bench.json
 cat $OUT/bench.json
-timeout -k 10 300 python3 bench.py --config C5 --no-cpu --steps 50 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -20 $OUT/bench_c5.err; exit 1; }
+timeout -k 10 300 python3 bench.py --config C5 --no-cpu --steps 200 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -20 $OUT/bench_c5.err; exit 1; }
 cat $OUT/bench_c5.json
 # compat mode (the GUI path): the train scene at three cell sizes, generated kernels, and its
 # kernel trace at cellsize 0.03
