@@ -980,7 +980,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     mpu_sync();
     const bool recs = work && !(p.debug & 2u);  // ablation bit 1: pass 1 only
     const uint32_t shard = d & (kShards - 1);
-    VertexRec* vq = p.vq + (size_t)shard * p.vShardCap;
+    VertexKey* vk = p.vk + (size_t)shard * p.vShardCap;
     TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
 
     // pass 2 (:703-762), one lane per new vertex r (batches of 64 dealt to the MPU's waves
@@ -1012,13 +1012,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
                 edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
                 const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
                 const uint32_t g = qv + r;
-                if (g < p.vShardCap) {  // pos holds the MPU origin until k_vertex writes the vertex
-                    vq[g].w = w;
-                    vq[g].vidKey = r | (key << 16);
-                    vq[g].pos[0] = o[0];
-                    vq[g].pos[1] = o[1];
-                    vq[g].pos[2] = o[2];
-                }
+                if (g < p.vShardCap) vk[g] = VertexKey{w, r | (key << 16)};
             }
         }
     }
@@ -1312,8 +1306,9 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             valid[n] = rr < count;
             if (!valid[n]) rr = first;
             rec[n] = (size_t)shard * p.vShardCap + rr;
-            const VertexRec R = p.vq[rec[n]];
-            const float o[3] = {R.pos[0], R.pos[1], R.pos[2]};  // the MPU origin (k_mpu)
+            const VertexKey R = p.vk[rec[n]];
+            float o[3];
+            mpu_origin(p, R.w + p.mpuBegin, o);  // the MPU origin, as k_mpu computed it
             wrec[n] = R.w;
             key[n] = R.vidKey >> 16;
             const int sx = key[n] & 7, sy = (key[n] >> 3) & 7, sz = (key[n] >> 6) & 7, ax = (key[n] >> 9) & 3;
@@ -1375,12 +1370,9 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
             const float scale = (0.5f - fa) / (fb - fa);
             if (valid[n] && j == 0) {  // into the record; k_finish adds normal and colour
-                VertexRec& out = p.vq[rec[n]];
-                out.pos[0] = ax0 + scale * (bx0 - ax0);
-                out.pos[1] = ay0 + scale * (by0 - ay0);
-                out.pos[2] = az0 + scale * (bz0 - az0);
-                // 1: p lies on its bracketing segment, inside the MPU box (no inf/NaN)
-                out.nrm[0] = (scale >= 0.0f && scale <= 1.0f) ? 1.0f : 0.0f;
+                // onSeg 1: p lies on its bracketing segment, inside the MPU box (no inf/NaN)
+                p.vp[rec[n]] = VertexPos{{ax0 + scale * (bx0 - ax0), ay0 + scale * (by0 - ay0), az0 + scale * (bz0 - az0)},
+                                         (scale >= 0.0f && scale <= 1.0f) ? 1.0f : 0.0f};
             }
         }
     }
@@ -1431,8 +1423,10 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         uint32_t rec = first + (uint32_t)lane;
         const bool valid = rec < count;
         if (!valid) rec = first;
-        const VertexRec R = p.vq[(size_t)shard * p.vShardCap + rec];
-        const uint32_t gi = (uint32_t)p.offs[R.w] + (R.vidKey & 0xffffu);
+        const size_t ri = (size_t)shard * p.vShardCap + rec;
+        const VertexKey K = p.vk[ri];
+        const VertexPos R = p.vp[ri];
+        const uint32_t gi = (uint32_t)p.offs[K.w] + (K.vidKey & 0xffffu);
         float c[3] = {0.0f, 0.0f, 0.0f};
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
         if (!(p.debug & 32u)) {  // ablation bit 5: no walks
@@ -1440,7 +1434,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
             // every normal sample; otherwise the wave's own box grown by delta
             CullMask cm{0ull, 0ull};
             if (p.cull) {
-                if (ballot(!(R.nrm[0] == 1.0f)) == 0ull) cm = cull_mask_mpus(p, R.w);
+                if (ballot(!(R.onSeg == 1.0f)) == 0ull) cm = cull_mask_mpus(p, K.w);
                 else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
             }
             // value + colour at p and the normal's per-point fieldValue at p + delta*e_a

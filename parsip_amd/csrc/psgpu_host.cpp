@@ -439,7 +439,8 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     PSGPU_CHECK(grow(c->passed, c->capPassed, n));
     PSGPU_CHECK(grow(c->mpuMasks, c->capMasks, 2 * n));
     PSGPU_CHECK(grow(c->offs, c->capOff, n + 1));
-    PSGPU_CHECK(grow(c->vq, c->capVq, (size_t)c->vShardCap * kShards));
+    PSGPU_CHECK(grow(c->vk, c->capVk, (size_t)c->vShardCap * kShards));
+    PSGPU_CHECK(grow(c->vp, c->capVp, (size_t)c->vShardCap * kShards));
     PSGPU_CHECK(grow(c->tq, c->capTq, (size_t)c->tShardCap * kShards));
     size_t capV2 = c->capV, capV3 = c->capV;
     PSGPU_CHECK(grow(c->pos, c->capV, (size_t)c->vcap * 3));
@@ -485,7 +486,8 @@ Params make_params(psgpu_ctx* c) {
     p.bound = (c->bound && c->jit && c->model.boundable) ? 1u : 0u;
     p.mpuMasks = c->mpuMasks;
     p.offs = c->offs;
-    p.vq = c->vq;
+    p.vk = c->vk;
+    p.vp = c->vp;
     p.vShardCap = c->vShardCap;
     p.tq = c->tq;
     p.tShardCap = c->tShardCap;
@@ -864,7 +866,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (c->jitPending && c->jitFut.valid()) c->jitFut.wait();
     c->jitFut = JitFuture();
     c->jit.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vq, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -890,11 +892,11 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
         c->pending = false;
         c->seenV = c->seenT = c->seenShardV = c->seenShardT = 0;
-        void* bufs[] = {c->vq, c->tq, c->pos, c->nrm, c->col, c->tris};
+        void* bufs[] = {c->vk, c->vp, c->tq, c->pos, c->nrm, c->col, c->tris};
         for (void* b : bufs)
             if (b) (void)hipFree(b);
-        c->vq = nullptr; c->tq = nullptr; c->pos = nullptr; c->nrm = nullptr; c->col = nullptr; c->tris = nullptr;
-        c->capVq = c->capTq = c->capV = c->capT = 0;
+        c->vk = nullptr; c->vp = nullptr; c->tq = nullptr; c->pos = nullptr; c->nrm = nullptr; c->col = nullptr; c->tris = nullptr;
+        c->capVk = c->capVp = c->capTq = c->capV = c->capT = 0;
         c->vcap = (uint32_t)value;
         c->tcap = (uint32_t)std::min<int64_t>(2 * value, 0xffffffffll);
         c->vShardCap = (uint32_t)std::max<int64_t>(16, value / kShards);

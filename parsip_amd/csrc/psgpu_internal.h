@@ -21,7 +21,8 @@ struct psgpu_ctx {
     using DevModel = psgpu::DevModel;
     using Params = psgpu::Params;
     using DevCounters = psgpu::DevCounters;
-    using VertexRec = psgpu::VertexRec;
+    using VertexKey = psgpu::VertexKey;
+    using VertexPos = psgpu::VertexPos;
     using TriRec = psgpu::TriRec;
     using CubeTablesDev = psgpu::CubeTablesDev;
     static constexpr int kNumKernels = psgpu::kNumKernels;
@@ -52,7 +53,7 @@ struct psgpu_ctx {
     bool pending = false;
     bool haveResult = false;
     // device buffers
-    size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVq = 0, capTq = 0, capV = 0, capT = 0;
+    size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVk = 0, capVp = 0, capTq = 0, capV = 0, capT = 0;
     uint32_t* pq = nullptr;         // sharded S1 survivor queues
     uint64_t* pqMask = nullptr;     // 2 words per queue entry (culling mask of the MPU box)
     size_t capPqMask = 0;
@@ -69,7 +70,8 @@ struct psgpu_ctx {
     uint64_t* mpuMasks = nullptr;
     size_t capMasks = 0;
     uint64_t* offs = nullptr;
-    VertexRec* vq = nullptr;
+    VertexKey* vk = nullptr;
+    VertexPos* vp = nullptr;
     TriRec* tq = nullptr;
     float* pos = nullptr;
     float* nrm = nullptr;

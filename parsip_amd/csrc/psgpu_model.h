@@ -141,11 +141,15 @@ struct DevModel {
 };
 
 // Compact-mesh work records written by the MPU kernel.
-struct VertexRec {       // 32 B: MPU slot in the range, vid | edge key << 16, then k_vertex's
-    uint32_t w;          // position and normal (k_finish places it in the compact mesh)
+// A vertex record in two arrays, so that each kernel moves only what it uses: k_mpu writes
+// the key (8 B), k_vertex reads it and writes the position (16 B), k_finish reads both.
+struct VertexKey {       // 8 B: MPU slot in the range, vid | edge key << 16
+    uint32_t w;
     uint32_t vidKey;     // vid | key << 16, key = sx | sy<<3 | sz<<6 | axis<<9
+};
+struct VertexPos {       // 16 B (k_vertex): the root, and 1 if it lies on its bracketing segment
     float pos[3];
-    float nrm[3];
+    float onSeg;
 };
 struct TriRec {          // 16 B
     uint32_t w;
@@ -216,7 +220,8 @@ struct Params {
     uint64_t* scanStatusNext;
     uint32_t scanBlocks;    // offsets-scan blocks (the first blocks of k_vertex)
     uint32_t scanChunks;    // kScanItems chunks per scan block
-    VertexRec* vq;          // kShards queues of vShardCap records
+    VertexKey* vk;          // kShards queues of vShardCap vertex records (keys ...
+    VertexPos* vp;          // ... and positions, same indexing)
     uint32_t vShardCap;
     TriRec* tq;             // kShards queues of tShardCap records
     uint32_t tShardCap;
