@@ -67,6 +67,30 @@ def test_reference_counts_and_golden_digests(gpu_poly, name):
     assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig
 
 
+def test_engines_pipelined_c3_golden():
+    """The bench's pipelining: 4 contexts take 12 C3 polygonizations in turn, queued without
+    host synchronisation (bench.py's timed loop); every context's last mesh equals the
+    committed oracle digests, so the queued runs do not disturb each other."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))["C3"]
+    model, cs, _ = synth.make_config("C3")
+    ps = [gpu.Polygonizer(0) for _ in range(4)]
+    try:
+        for p in ps:
+            p.set_model(model)
+            p.run(cs)  # sizes the buffers
+        for k in range(12):
+            ps[k % 4].polygonize(cs)
+        for p in ps:
+            p.finish()
+            gm, gs = p.download(), p.stats()
+            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+            assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig
+    finally:
+        for p in ps:
+            p.close()
+
+
 def test_c3_full_size(gpu_poly, oracle):
     """Headline workload (256^3, 32 prims, pruning live) against the oracle, in full."""
     model, cs, _ = synth.make_config("C3")
