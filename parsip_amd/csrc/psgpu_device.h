@@ -642,10 +642,21 @@ __device__ __forceinline__ void span_end(const Params& p, int K, uint64_t t0) {
     }
 
 // ---------------------------------------------------------------------------
+// Exact m / d from a multiply-high by floor((2^32 - 1) / d): the estimate never exceeds the
+// quotient and falls short of it by at most 2.
+__device__ __forceinline__ uint32_t div_by(uint32_t m, uint32_t d, uint32_t magic, uint32_t* rem) {
+    uint32_t q = __umulhi(m, magic);
+    uint32_t r = m - q * d;
+    if (r >= d) { ++q; r -= d; }
+    if (r >= d) { ++q; r -= d; }
+    *rem = r;
+    return q;
+}
+
 __device__ __forceinline__ void mpu_origin(const Params& p, uint32_t m, float o[3]) {
-    const uint32_t k = m % p.dims[2];
-    const uint32_t j = (m / p.dims[2]) % p.dims[1];
-    const uint32_t i = m / (p.dims[2] * p.dims[1]);
+    uint32_t k, jk;
+    const uint32_t i = div_by(m, p.dims[2] * p.dims[1], p.divMagic[1], &jk);
+    const uint32_t j = div_by(jk, p.dims[2], p.divMagic[0], &k);
     o[0] = p.lo[0] + (float)i * p.side;
     o[1] = p.lo[1] + (float)j * p.side;
     o[2] = p.lo[2] + (float)k * p.side;

@@ -461,6 +461,8 @@ Params make_params(psgpu_ctx* c) {
     p.lo[1] = c->primsHost.bboxLo.y;
     p.lo[2] = c->primsHost.bboxLo.z;
     for (int a = 0; a < 3; ++a) p.dims[a] = c->dims[a];
+    p.divMagic[0] = p.dims[2] ? 0xffffffffu / p.dims[2] : 0u;
+    p.divMagic[1] = (p.dims[2] * p.dims[1]) ? 0xffffffffu / (p.dims[2] * p.dims[1]) : 0u;
     p.mpuBegin = c->mpuBegin;
     p.mpuCount = c->mpuCount;
     p.cull = (uint32_t)c->cull;

@@ -199,6 +199,7 @@ struct Params {
     float side;         // cellsize * 7.0f (MPU side)
     float lo[3];        // scene bboxLo
     uint32_t dims[3];   // MPU lattice
+    uint32_t divMagic[2];  // floor((2^32 - 1) / d) for d = dims[2], dims[1] * dims[2] (mpu_origin)
     uint32_t mpuBegin;
     uint32_t mpuCount;
     uint32_t cull;      // exact per-wave primitive culling enabled
