@@ -1051,7 +1051,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
                 v[sv] = edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax];
             }
             const uint32_t g = qt + r;
-            if (g < p.tShardCap) tq[g] = TriRec{w, r, v[0] | (v[1] << 16), v[2]};
+            if (g < p.tShardCap) tq[g] = TriRec{w, r | (v[0] << 11) | ((v[1] & 1023u) << 22), (v[1] >> 10) | (v[2] << 1)};
         }
     }
 }
@@ -1489,12 +1489,12 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         if (t >= count) continue;
         const TriRec R = p.tq[(size_t)shard * p.tShardCap + t];
         const uint64_t o = p.offs[R.w];
-        const uint32_t gt = (uint32_t)(o >> 32) + R.tlocal;
+        const uint32_t gt = (uint32_t)(o >> 32) + (R.a & 2047u);
         const uint32_t base = (uint32_t)o;
         if (gt >= p.tCap) continue;  // finish() grows and re-runs
-        p.tris[gt * 3 + 0] = base + (R.v01 & 0xffffu);
-        p.tris[gt * 3 + 1] = base + (R.v01 >> 16);
-        p.tris[gt * 3 + 2] = base + R.v2;
+        p.tris[gt * 3 + 0] = base + ((R.a >> 11) & 2047u);
+        p.tris[gt * 3 + 1] = base + ((R.a >> 22) | ((R.b & 1u) << 10));
+        p.tris[gt * 3 + 2] = base + ((R.b >> 1) & 2047u);
     }
 }
 

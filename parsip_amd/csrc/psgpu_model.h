@@ -151,11 +151,10 @@ struct VertexPos {       // 16 B (k_vertex): the root, and 1 if it lies on its b
     float pos[3];
     float onSeg;
 };
-struct TriRec {          // 16 B
-    uint32_t w;
-    uint32_t tlocal;
-    uint32_t v01;        // v0 | v1 << 16
-    uint32_t v2;
+struct TriRec {          // 12 B: MPU slot, then 11-bit fields (an MPU has at most 1,715
+    uint32_t w;          // triangles and 1,344 edges): tlocal | v0 << 11 | v1 << 22 (low 10
+    uint32_t a;          // bits), then v1 >> 10 | v2 << 1
+    uint32_t b;
 };
 
 // Device-side scalars of one polygonization.
