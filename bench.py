@@ -276,7 +276,7 @@ class Engine:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
