@@ -274,6 +274,28 @@ def test_gpu_rejects_unsupported_nodes(gui_ctx):
 
 
 @pytest.mark.gpu
+def test_gpu_structural_edit_does_not_wait():
+    """A structural edit while the previous tree's kernels still compile returns at once (the
+    old compile finishes in the background); the new tree's kernels then serve, bit-exact."""
+    import time
+
+    p = gui.ParsipOptimized(0, jit=1)
+    try:
+        _, tree_a = gui.compact_blobtree(random_tree(31, n_prims=14))
+        _, tree_b = gui.compact_blobtree(random_tree(32, n_prims=14))
+        t0 = time.perf_counter()
+        p.set_tree(tree_a)
+        p.set_tree(tree_b)
+        assert time.perf_counter() - t0 < 2.0
+        assert p.jit_status(wait=True) == gui.JIT_ACTIVE
+        p.jit_mode = 2
+        gm, om = _both(p, tree_b, 0.06)
+        assert_gui_mesh_equal(gm, om, "after the edit")
+    finally:
+        p.close()
+
+
+@pytest.mark.gpu
 def test_gpu_run_polygonizer_api(train):
     root, _ = train
     p = gui.Run_Polygonizer(root, 0.25)
