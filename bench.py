@@ -344,10 +344,23 @@ def main():
     exchange = None
     if strong:
         if pinned is None:  # one communicator per engine: its all-gathers stay on its stream
-            for e in engines:
-                uid = grp.broadcast_bytes(gpu.comm_unique_id() if grp.rank == 0 else None)
-                e.comm = gpu.Comm(e.obj, uid, grp.world, grp.rank)
-            exchange = "rccl all-gather of 8 words per rank per step (library stream)"
+            err = None
+            try:
+                for e in engines:
+                    uid = grp.broadcast_bytes(gpu.comm_unique_id() if grp.rank == 0 else None)
+                    e.comm = gpu.Comm(e.obj, uid, grp.world, grp.rank)
+            except gpu.PsgpuError as x:  # every rank learns whether all communicators exist
+                err = x
+            if grp.max(1.0 if err else 0.0) > 0.0:
+                for e in engines:
+                    if e.comm:
+                        e.comm.close()
+                    e.comm = None
+                print(f"bench.py rank {grp.rank}: RCCL communicators unavailable ({err}); the totals "
+                      "go over gloo after the timed steps", file=sys.stderr)
+                exchange = "gloo all-gather after the timed steps (RCCL communicator creation failed)"
+            else:
+                exchange = "rccl all-gather of 8 words per rank per step (library stream)"
         else:
             exchange = "gloo all-gather after the timed steps (ranks share one device: RCCL needs distinct GPUs)"
 
