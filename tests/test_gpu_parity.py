@@ -91,6 +91,32 @@ def test_engines_pipelined_c3_golden():
             p.close()
 
 
+def test_engines_different_models_interleaved():
+    """Contexts holding different trees (C2, C3: different generated kernels) queued in turn
+    without host sync each reproduce their own oracle digests."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    digs = json.load(open(os.path.join(gdir, "oracle_digests.json")))
+    cfg = ["C2", "C3", "C2", "C3"]
+    ps = [gpu.Polygonizer(0) for _ in cfg]
+    try:
+        css = []
+        for p, name in zip(ps, cfg):
+            model, cs, _ = synth.make_config(name)
+            p.set_model(model)
+            p.run(cs)
+            css.append(cs)
+        for k in range(16):
+            ps[k % 4].polygonize(css[k % 4])
+        for p, name in zip(ps, cfg):
+            p.finish()
+            gm, gs = p.download(), p.stats()
+            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+            assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == digs[name], name
+    finally:
+        for p in ps:
+            p.close()
+
+
 def test_c3_full_size(gpu_poly, oracle):
     """Headline workload (256^3, 32 prims, pruning live) against the oracle, in full."""
     model, cs, _ = synth.make_config("C3")
