@@ -180,10 +180,11 @@ struct DevCounters {
 };
 
 #ifndef PSGPU_MPU_WAVES
-#define PSGPU_MPU_WAVES 2  // waves per S1 survivor in k_mpu (1, 2 or 4): each walks 8 / W of the
+#define PSGPU_MPU_WAVES 1  // waves per S1 survivor in k_mpu (1, 2 or 4): each walks 8 / W of the
                            // 8 x-slices of the S2 cache and takes every W-th batch of records,
                            // so a heavy MPU's critical path is ~1/W of one wave doing it all.
                            // Host and device must agree (build.py and the JIT pass the same value).
+                           // C3 ms/step on one box: W=1 0.0624, W=2 0.0669, W=4 0.0722.
 #endif
 constexpr int kMpuWaves = PSGPU_MPU_WAVES;
 constexpr int kMpusPerBlock = 4 / kMpuWaves;  // k_mpu blocks are 4 waves
