@@ -1427,6 +1427,56 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     stage_shard_counts(p, 1, sCnt);            // ShardCtr::v
     stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
     __syncthreads();
+#if PSGPU_FIN_VPW == 16
+    // a quad of lanes per vertex: lane j of the quad walks point j (p, p + delta e_x,
+    // p + delta e_y, p + delta e_z) with the same per-point pruning (GROUP 1) as the
+    // 4-point walk below, so every value is the same; lanes 0-2 of the quad then write
+    // component j of position, normal and colour
+    const ShardBatches sv(sCnt, p.vShardCap, 16);
+    const int qj = lane & 3;
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sv.locate(batch, &shard, &first, &count);
+        uint32_t rec = first + (uint32_t)(lane >> 2);
+        const bool valid = rec < count;
+        if (!valid) rec = first;
+        const size_t ri = (size_t)shard * p.vShardCap + rec;
+        const VertexKey K = p.vk[ri];
+        const VertexPos R = p.vp[ri];
+        const uint32_t gi = (uint32_t)p.offs[K.w] + (K.vidKey & 0xffffu);
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        if (!(p.debug & 32u)) {  // ablation bit 5: no walks
+            CullMask cm{0ull, 0ull};
+            if (p.cull) {
+                if (ballot(!(R.onSeg == 1.0f)) == 0ull) cm = cull_mask_mpus(p, K.w);
+                else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
+            }
+            const float qx = qj == 1 ? R.pos[0] + delta : R.pos[0];
+            const float qy = qj == 2 ? R.pos[1] + delta : R.pos[1];
+            const float qz = qj == 3 ? R.pos[2] + delta : R.pos[2];
+            float c4[3];
+            const float g = ev.template eval<1, true>(qx, qy, qz, cm, c4);
+            c[0] = quad_bcast<0>(c4[0]);
+            c[1] = quad_bcast<0>(c4[1]);
+            c[2] = quad_bcast<0>(c4[2]);
+            const float vtx = quad_bcast<0>(g);
+            nx = (quad_bcast<1>(g) - vtx) * inv;
+            ny = (quad_bcast<2>(g) - vtx) * inv;
+            nz = (quad_bcast<3>(g) - vtx) * inv;
+            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);
+            nx = nx * im;
+            ny = ny * im;
+            nz = nz * im;
+        }
+        if (valid && qj < 3 && gi < p.vCap) {  // past vCap: finish() grows and re-runs
+            const uint32_t o = gi * 3 + (uint32_t)qj;
+            p.pos[o] = qj == 0 ? R.pos[0] : (qj == 1 ? R.pos[1] : R.pos[2]);
+            p.nrm[o] = qj == 0 ? nx : (qj == 1 ? ny : nz);
+            p.col[o] = qj == 0 ? c[0] : (qj == 1 ? c[1] : c[2]);
+        }
+    }
+#else
     const ShardBatches sv(sCnt, p.vShardCap, 64);
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
         uint32_t shard, first, count;
@@ -1480,6 +1530,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
             p.col[gi * 3 + 2] = c[2];
         }
     }
+#endif
     if (p.debug & 64u) return;  // ablation bit 6: no triangles
     const ShardBatches sb(sCnt + kShards, p.tShardCap, 64);
     for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
