@@ -1389,11 +1389,13 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     }
 }
 
-// Finish: per vertex (one lane per vertex, 64 per wave) fieldValueAndColor's value and
-// colour walk (PS_Polygonizer.cpp:777-778, 1378-1551) and the three normal samples
-// (:780-781, 1598-1622), then the triangle records -> global vertex ids.  Runs after
-// k_vertex wrote the positions.
-template <class EV>
+// Finish: per vertex fieldValueAndColor's value and colour walk (PS_Polygonizer.cpp:777-778,
+// 1378-1551) and the three normal samples (:780-781, 1598-1622), then the triangle records
+// -> global vertex ids.  Runs after k_vertex wrote the positions.  VPW 64: one lane per
+// vertex walking its 4 points; VPW 16: a quad of lanes per vertex, one point each (a
+// quarter of the walk per wave: shorter spans when the vertices do not fill the persistent
+// grid, e.g. a small rank share; more total work otherwise).  Same values either way.
+template <class EV, int VPW = 64>
 __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
@@ -1427,7 +1429,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     stage_shard_counts(p, 1, sCnt);            // ShardCtr::v
     stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
     __syncthreads();
-#if PSGPU_FIN_VPW == 16
+if constexpr (VPW == 16) {
     // a quad of lanes per vertex: lane j of the quad walks point j (p, p + delta e_x,
     // p + delta e_y, p + delta e_z) with the same per-point pruning (GROUP 1) as the
     // 4-point walk below, so every value is the same; lanes 0-2 of the quad then write
@@ -1476,7 +1478,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
             p.col[o] = qj == 0 ? c[0] : (qj == 1 ? c[1] : c[2]);
         }
     }
-#else
+} else {
     const ShardBatches sv(sCnt, p.vShardCap, 64);
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
         uint32_t shard, first, count;
@@ -1530,7 +1532,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
             p.col[gi * 3 + 2] = c[2];
         }
     }
-#endif
+}
     if (p.debug & 64u) return;  // ablation bit 6: no triangles
     const ShardBatches sb(sCnt + kShards, p.tShardCap, 64);
     for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {

@@ -520,10 +520,20 @@ hipError_t launch_jit(hipFunction_t f, uint32_t blocks, uint32_t threads, size_t
 // One polygonization = 5 kernels, no copies or fills: k_precheck resets the counters,
 // k_finish publishes them to mapped host memory.
 // The five launches of one polygonization (shared by direct launch and graph capture).
+// k_finish layout for the next run: a quad of lanes per vertex when the last run's vertices,
+// 16 per wave, fit the persistent grid's waves in one pass (each wave then walks a quarter
+// of what a 64-vertex wave does); otherwise one lane per vertex (fewer waves in total).
+bool finish_quad(const psgpu_ctx* c) {
+    if (c->finishQuad != 2) return c->finishQuad == 1;
+    const uint64_t waves = (uint64_t)c->numCUs * (uint64_t)c->finishBlocksPerCU * 4u;
+    return c->lastV > 0 && (uint64_t)c->lastV <= 16u * waves;
+}
+
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
     const uint32_t persistF = (uint32_t)(c->numCUs * c->finishBlocksPerCU);
+    const bool quad = finish_quad(c);
     JitKernels* J = c->jit.get();
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
@@ -537,8 +547,8 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(J->vertex, gridV, 256, 0, s, p));
     else PSGPU_CHECK(launch_vertex(p, s, gridV));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-    if (J) PSGPU_CHECK(launch_jit(J->finish, persistF, 256, 0, s, p));
-    else PSGPU_CHECK(launch_finish(p, s, persistF));
+    if (J) PSGPU_CHECK(launch_jit(quad ? J->finishQ : J->finish, persistF, 256, 0, s, p));
+    else PSGPU_CHECK(launch_finish(p, s, persistF, quad));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
     return PSGPU_RET_SUCCESS;
 }
@@ -575,7 +585,8 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         return rc;
     }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
-    const uint32_t shape[3] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs};
+    const uint32_t shape[4] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
+                               finish_quad(c) ? 1u : 0u};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
           memcmp(g.shape, shape, sizeof(shape)) == 0)) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -907,6 +918,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     }
     else if (option == PSGPU_OPT_VERTEX_BLOCKS_PER_CU && value >= 1 && value <= 32) c->vertexBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_FINISH_BLOCKS_PER_CU && value >= 1 && value <= 32) c->finishBlocksPerCU = (int)value;
+    else if (option == PSGPU_OPT_FINISH_QUAD && value >= 0 && value <= 2) c->finishQuad = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;
@@ -1020,6 +1032,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             }
             const bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
             c->lastQueued = Q;
+            c->lastV = V;
             c->haveQueued = c->mpuCount > 0;
             c->seenV = std::max(c->seenV, V);
             c->seenT = std::max(c->seenT, T);

@@ -44,6 +44,8 @@ struct psgpu_ctx {
     int debug = 0;
     int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
     int finishBlocksPerCU = 8;
+    int finishQuad = 2;  // PSGPU_OPT_FINISH_QUAD: 0 never, 1 always, 2 by the last run's vertex count
+    uint32_t lastV = 0;  // vertices of the last finished run (0: none yet)
     int timing = 0;
     // geometry of the last run
     float cs = 0.0f;
@@ -93,7 +95,7 @@ struct psgpu_ctx {
         hipGraphExec_t exec = nullptr;
         JitKernels* jit = nullptr;
         Params key{};
-        uint32_t shape[3] = {0, 0, 0};
+        uint32_t shape[4] = {0, 0, 0, 0};
     } graphs[2];
     float lastMs[kNumKernels] = {};
     PsMeshInfo info{};

@@ -13,7 +13,8 @@ namespace psgpu {
 
 struct JitKernels {
     hipModule_t mod = nullptr;
-    hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, finish = nullptr, probe = nullptr;
+    hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, finish = nullptr, finishQ = nullptr,
+                  probe = nullptr;
 };
 
 extern const char* const kJitArch;  // "gfx950"

@@ -48,7 +48,11 @@ __global__ void __launch_bounds__(256) k_probe(Params p, const float* __restrict
 
 __global__ void __launch_bounds__(256) k_finish(Params p) {
     extern __shared__ __attribute__((aligned(16))) float flds[];
-    PSGPU_STAMPED(3, item_, finish_body<InterpEval>(p, flds));
+    PSGPU_STAMPED(3, item_, (finish_body<InterpEval, 64>(p, flds)));
+}
+__global__ void __launch_bounds__(256) k_finish_q(Params p) {
+    extern __shared__ __attribute__((aligned(16))) float flds[];
+    PSGPU_STAMPED(3, item_, (finish_body<InterpEval, 16>(p, flds)));
 }
 
 // Gathered parts of one grid (psgpu_group_gather): a part's triangles get its vertex
@@ -95,8 +99,9 @@ hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks) {
     hipLaunchKernelGGL(k_vertex, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
-hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks) {
-    hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
+hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks, bool quad) {
+    if (quad) hipLaunchKernelGGL(k_finish_q, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
+    else hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
 hipError_t launch_probe(const Params& p, hipStream_t s, const float* xyz, float* out, float* col, uint32_t n,

@@ -187,10 +187,6 @@ struct DevCounters {
                            // C3 ms/step on one box: W=1 0.0624, W=2 0.0669, W=4 0.0722.
 #endif
 constexpr int kMpuWaves = PSGPU_MPU_WAVES;
-#ifndef PSGPU_FIN_VPW
-#define PSGPU_FIN_VPW 64  // k_finish vertices per wave: 64 (one lane per vertex walking its 4 points)
-                          // or 16 (a quad of lanes per vertex, one point each: shorter waves)
-#endif
 constexpr int kMpusPerBlock = 4 / kMpuWaves;  // k_mpu blocks are 4 waves
 constexpr int kNumStampKernels = 4;  // k_precheck, k_mpu, k_vertex, k_finish
 constexpr int kSpanLanes = 64;       // {min start, max end} pairs per kernel per run (PSGPU_OPT_SPANS)

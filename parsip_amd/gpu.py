@@ -75,6 +75,7 @@ OPT_BOUND = 10
 OPT_JIT_ASYNC = 11
 OPT_STAMPS = 12
 OPT_SPANS = 13
+OPT_FINISH_QUAD = 14
 STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
 BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3

@@ -67,6 +67,29 @@ def test_reference_counts_and_golden_digests(gpu_poly, name):
     assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig
 
 
+@pytest.mark.parametrize("name", ["C2", "C3"])
+@pytest.mark.parametrize("jit", [0, 1])
+def test_finish_layouts_golden(gpu_poly, name, jit):
+    """k_finish one lane per vertex (OPT_FINISH_QUAD 0), a quad of lanes per vertex (1) and
+    the per-run choice (2; the second run sees the first run's vertex count) all reproduce
+    the committed oracle digests."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
+    model, cs, _ = synth.make_config(name)
+    gpu_poly.set_option(gpu.OPT_JIT, jit)
+    gpu_poly.set_model(model)
+    try:
+        for mode in (0, 1, 2, 2):
+            gpu_poly.set_option(gpu.OPT_FINISH_QUAD, mode)
+            gpu_poly.run(cs)
+            gm, gs = gpu_poly.download(), gpu_poly.stats()
+            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+            assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig, (name, jit, mode)
+    finally:
+        gpu_poly.set_option(gpu.OPT_FINISH_QUAD, 2)
+        gpu_poly.set_option(gpu.OPT_JIT, 1)
+
+
 def test_engines_pipelined_c3_golden():
     """The bench's pipelining: 4 contexts take 12 C3 polygonizations in turn, queued without
     host synchronisation (bench.py's timed loop); every context's last mesh equals the
