@@ -258,9 +258,10 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_SPANS        13   /* > 0: the next this-many runs record each kernel's span on the
                                        device clock (first wave start, last wave end; 100 MHz) */
 #define PSGPU_OPT_FINISH_QUAD  14   /* k_finish layout: 0 one lane per vertex (64 per wave), 1 a quad
-                                       of lanes per vertex (16 per wave), 2 (default) the quad when
-                                       the last run's vertices fill at most one pass of the persistent
-                                       grid (small rank shares); identical output */
+                                       of lanes per vertex (16 per wave), 3 a pair of lanes (32 per
+                                       wave), 2 (default) the fewest vertices per wave whose waves
+                                       hold the last run's vertices in one pass of the persistent
+                                       grid (16 or 32; else 64: small rank shares); identical output */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the
                                        specialised kernels on a host thread while the interpreter
                                        serves polygonizations (bit-identical output); 0: block */

@@ -1478,6 +1478,66 @@ if constexpr (VPW == 16) {
             p.col[o] = qj == 0 ? c[0] : (qj == 1 ? c[1] : c[2]);
         }
     }
+} else if constexpr (VPW == 32) {
+    // a pair of lanes per vertex: lane j of the pair walks points 2j, 2j + 1 of
+    // {p, p + delta e_x, p + delta e_y, p + delta e_z} (per-point pruning, as above); the
+    // partner's two values come over DPP; lane j writes component j, lane 0 also component 2
+    const ShardBatches sv(sCnt, p.vShardCap, 32);
+    const int pj = lane & 1;
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sv.locate(batch, &shard, &first, &count);
+        uint32_t rec = first + (uint32_t)(lane >> 1);
+        const bool valid = rec < count;
+        if (!valid) rec = first;
+        const size_t ri = (size_t)shard * p.vShardCap + rec;
+        const VertexKey K = p.vk[ri];
+        const VertexPos R = p.vp[ri];
+        const uint32_t gi = (uint32_t)p.offs[K.w] + (K.vidKey & 0xffffu);
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        if (!(p.debug & 32u)) {  // ablation bit 5: no walks
+            CullMask cm{0ull, 0ull};
+            if (p.cull) {
+                if (ballot(!(R.onSeg == 1.0f)) == 0ull) cm = cull_mask_mpus(p, K.w);
+                else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
+            }
+            // lane 0: p, p + delta e_x; lane 1: p + delta e_y, p + delta e_z
+            const float qx[2] = {R.pos[0], pj == 0 ? R.pos[0] + delta : R.pos[0]};
+            const float qy[2] = {pj == 1 ? R.pos[1] + delta : R.pos[1], R.pos[1]};
+            const float qz[2] = {R.pos[2], pj == 1 ? R.pos[2] + delta : R.pos[2]};
+            float g[2], c6[6];
+            ev.template evaln<1, true, 2>(qx, qy, qz, cm, g, c6);
+            const float o0 = PSGPU_DPP_F(g[0], 0xB1), o1 = PSGPU_DPP_F(g[1], 0xB1);
+            const float oc0 = PSGPU_DPP_F(c6[0], 0xB1), oc1 = PSGPU_DPP_F(c6[1], 0xB1),
+                        oc2 = PSGPU_DPP_F(c6[2], 0xB1);
+            c[0] = pj == 0 ? c6[0] : oc0;
+            c[1] = pj == 0 ? c6[1] : oc1;
+            c[2] = pj == 0 ? c6[2] : oc2;
+            const float vtx = pj == 0 ? g[0] : o0;
+            const float g1 = pj == 0 ? g[1] : o1;
+            const float g2 = pj == 0 ? o0 : g[0];
+            const float g3 = pj == 0 ? o1 : g[1];
+            nx = (g1 - vtx) * inv;
+            ny = (g2 - vtx) * inv;
+            nz = (g3 - vtx) * inv;
+            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);
+            nx = nx * im;
+            ny = ny * im;
+            nz = nz * im;
+        }
+        if (valid && gi < p.vCap) {  // past vCap: finish() grows and re-runs
+            const uint32_t o = gi * 3 + (uint32_t)pj;
+            p.pos[o] = pj == 0 ? R.pos[0] : R.pos[1];
+            p.nrm[o] = pj == 0 ? nx : ny;
+            p.col[o] = pj == 0 ? c[0] : c[1];
+            if (pj == 0) {
+                p.pos[gi * 3 + 2] = R.pos[2];
+                p.nrm[gi * 3 + 2] = nz;
+                p.col[gi * 3 + 2] = c[2];
+            }
+        }
+    }
 } else {
     const ShardBatches sv(sCnt, p.vShardCap, 64);
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {

@@ -520,20 +520,26 @@ hipError_t launch_jit(hipFunction_t f, uint32_t blocks, uint32_t threads, size_t
 // One polygonization = 5 kernels, no copies or fills: k_precheck resets the counters,
 // k_finish publishes them to mapped host memory.
 // The five launches of one polygonization (shared by direct launch and graph capture).
-// k_finish layout for the next run: a quad of lanes per vertex when the last run's vertices,
-// 16 per wave, fit the persistent grid's waves in one pass (each wave then walks a quarter
-// of what a 64-vertex wave does); otherwise one lane per vertex (fewer waves in total).
-bool finish_quad(const psgpu_ctx* c) {
-    if (c->finishQuad != 2) return c->finishQuad == 1;
+// k_finish layout for the next run (vertices per wave): a quad of lanes per vertex (16) when
+// the last run's vertices, 16 per wave, fit the persistent grid's waves in one pass (each
+// wave then walks a quarter of what a 64-vertex wave does), else a pair of lanes (32) when
+// they do 32 per wave, otherwise one lane per vertex (64: fewest waves in total).
+int finish_vpw(const psgpu_ctx* c) {
+    if (c->finishQuad == 0) return 64;
+    if (c->finishQuad == 1) return 16;
+    if (c->finishQuad == 3) return 32;
     const uint64_t waves = (uint64_t)c->numCUs * (uint64_t)c->finishBlocksPerCU * 4u;
-    return c->lastV > 0 && (uint64_t)c->lastV <= 16u * waves;
+    if (c->lastV == 0) return 64;
+    if ((uint64_t)c->lastV <= 16u * waves) return 16;
+    if ((uint64_t)c->lastV <= 32u * waves) return 32;
+    return 64;
 }
 
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
     const uint32_t persistF = (uint32_t)(c->numCUs * c->finishBlocksPerCU);
-    const bool quad = finish_quad(c);
+    const int vpw = finish_vpw(c);
     JitKernels* J = c->jit.get();
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
@@ -547,8 +553,8 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(J->vertex, gridV, 256, 0, s, p));
     else PSGPU_CHECK(launch_vertex(p, s, gridV));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-    if (J) PSGPU_CHECK(launch_jit(quad ? J->finishQ : J->finish, persistF, 256, 0, s, p));
-    else PSGPU_CHECK(launch_finish(p, s, persistF, quad));
+    if (J) PSGPU_CHECK(launch_jit(vpw == 16 ? J->finishQ : (vpw == 32 ? J->finishP : J->finish), persistF, 256, 0, s, p));
+    else PSGPU_CHECK(launch_finish(p, s, persistF, vpw));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
     return PSGPU_RET_SUCCESS;
 }
@@ -586,7 +592,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
     const uint32_t shape[4] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
-                               finish_quad(c) ? 1u : 0u};
+                               (uint32_t)finish_vpw(c)};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
           memcmp(g.shape, shape, sizeof(shape)) == 0)) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -918,7 +924,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     }
     else if (option == PSGPU_OPT_VERTEX_BLOCKS_PER_CU && value >= 1 && value <= 32) c->vertexBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_FINISH_BLOCKS_PER_CU && value >= 1 && value <= 32) c->finishBlocksPerCU = (int)value;
-    else if (option == PSGPU_OPT_FINISH_QUAD && value >= 0 && value <= 2) c->finishQuad = (int)value;
+    else if (option == PSGPU_OPT_FINISH_QUAD && value >= 0 && value <= 3) c->finishQuad = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;

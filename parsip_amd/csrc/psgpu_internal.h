@@ -44,7 +44,7 @@ struct psgpu_ctx {
     int debug = 0;
     int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
     int finishBlocksPerCU = 8;
-    int finishQuad = 2;  // PSGPU_OPT_FINISH_QUAD: 0 never, 1 always, 2 by the last run's vertex count
+    int finishQuad = 2;  // PSGPU_OPT_FINISH_QUAD: 0 one lane, 1 a quad, 3 a pair of lanes per vertex, 2 by the last run's vertex count
     uint32_t lastV = 0;  // vertices of the last finished run (0: none yet)
     int timing = 0;
     // geometry of the last run

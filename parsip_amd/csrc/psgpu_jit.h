@@ -13,7 +13,7 @@ namespace psgpu {
 
 struct JitKernels {
     hipModule_t mod = nullptr;
-    hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, finish = nullptr, finishQ = nullptr,
+    hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, finish = nullptr, finishQ = nullptr, finishP = nullptr,
                   probe = nullptr;
 };
 

@@ -54,6 +54,10 @@ __global__ void __launch_bounds__(256) k_finish_q(Params p) {
     extern __shared__ __attribute__((aligned(16))) float flds[];
     PSGPU_STAMPED(3, item_, (finish_body<InterpEval, 16>(p, flds)));
 }
+__global__ void __launch_bounds__(256) k_finish_p(Params p) {
+    extern __shared__ __attribute__((aligned(16))) float flds[];
+    PSGPU_STAMPED(3, item_, (finish_body<InterpEval, 32>(p, flds)));
+}
 
 // Gathered parts of one grid (psgpu_group_gather): a part's triangles get its vertex
 // base added to their ids and its MPU offsets (V | T << 32) its (vertex, triangle)
@@ -99,8 +103,9 @@ hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks) {
     hipLaunchKernelGGL(k_vertex, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }
-hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks, bool quad) {
-    if (quad) hipLaunchKernelGGL(k_finish_q, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
+hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks, int vpw) {
+    if (vpw == 16) hipLaunchKernelGGL(k_finish_q, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
+    else if (vpw == 32) hipLaunchKernelGGL(k_finish_p, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     else hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(256), walk_lds_bytes(p.slotsPerLane), s, p);
     return hipGetLastError();
 }

@@ -14,7 +14,7 @@ size_t precheck_lds_bytes(uint32_t slots);
 hipError_t launch_precheck(const Params& p, hipStream_t s);
 hipError_t launch_mpu(const Params& p, hipStream_t s);
 hipError_t launch_vertex(const Params& p, hipStream_t s, uint32_t blocks);
-hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks, bool quad);
+hipError_t launch_finish(const Params& p, hipStream_t s, uint32_t blocks, int vpw);  // 64, 32 or 16 vertices per wave
 hipError_t launch_probe(const Params& p, hipStream_t s, const float* xyz, float* out, float* col, uint32_t n,
                         int mode);
 // tris[0..nTri) += vBase; offs[0..nOff) += offBase (gathered parts, psgpu_group.cpp)

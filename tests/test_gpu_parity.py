@@ -70,8 +70,8 @@ def test_reference_counts_and_golden_digests(gpu_poly, name):
 @pytest.mark.parametrize("name", ["C2", "C3"])
 @pytest.mark.parametrize("jit", [0, 1])
 def test_finish_layouts_golden(gpu_poly, name, jit):
-    """k_finish one lane per vertex (OPT_FINISH_QUAD 0), a quad of lanes per vertex (1) and
-    the per-run choice (2; the second run sees the first run's vertex count) all reproduce
+    """k_finish one lane per vertex (OPT_FINISH_QUAD 0), a quad (1) or a pair (3) of lanes per
+    vertex and the per-run choice (2; the second run sees the first run's vertex count) all reproduce
     the committed oracle digests."""
     gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
@@ -79,7 +79,7 @@ def test_finish_layouts_golden(gpu_poly, name, jit):
     gpu_poly.set_option(gpu.OPT_JIT, jit)
     gpu_poly.set_model(model)
     try:
-        for mode in (0, 1, 2, 2):
+        for mode in (0, 1, 3, 2, 2):
             gpu_poly.set_option(gpu.OPT_FINISH_QUAD, mode)
             gpu_poly.run(cs)
             gm, gs = gpu_poly.download(), gpu_poly.stats()
