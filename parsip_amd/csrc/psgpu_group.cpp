@@ -503,7 +503,7 @@ void psgpu_comm_destroy(psgpu_comm* m) {
 }
 
 // Enqueue the exchange of the context's last polygonization (its k_finish totals) on the
-// context's stream: ncclAllGather of 8 words per rank, then a copy to pinned memory.
+// context's stream: ncclAllGather of 8 words per rank (psgpu_comm_result copies them to the host).
 int psgpu_comm_exchange(psgpu_comm* m, psgpu_ctx* ctx) {
     if (!m || !ctx || ctx->device != m->device) return PSGPU_RET_PARAM_ERROR;
     int rc = set_device(ctx);
@@ -511,8 +511,6 @@ int psgpu_comm_exchange(psgpu_comm* m, psgpu_ctx* ctx) {
     hipStream_t s = ctx->runStream ? ctx->runStream : ctx->stream;
     rc = nccl_fail(ncclAllGather(ctx->totals, m->gathered, 8, ncclUint32, m->comm, s), "ncclAllGather");
     if (rc != PSGPU_RET_SUCCESS) return rc;
-    PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, (size_t)m->nranks * 8 * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, s));
     m->pending = true;
     m->ctx = ctx;
     m->group = nullptr;
@@ -551,8 +549,6 @@ int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
     PSGPU_CHECK(launch_sum_totals(tp, g->sumTotals, s0));
     rc = nccl_fail(ncclAllGather(g->sumTotals, m->gathered, 8, ncclUint32, m->comm, s0), "ncclAllGather");
     if (rc != PSGPU_RET_SUCCESS) return rc;
-    PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, (size_t)m->nranks * 8 * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, s0));
     m->pending = true;
     m->ctx = c0;
     m->group = g;
@@ -569,12 +565,17 @@ int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut
     int rc = m->group ? psgpu_group_finish(m->group, &mine, nullptr) : psgpu_finish(c, &mine);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     hipStream_t s = c->runStream ? c->runStream : c->stream;
+    // the gathered totals of the last exchange come to the host only here (not per step:
+    // one HIP call less on the host's enqueue path, which bounds small rank shares)
+    const size_t gb = (size_t)m->nranks * 8 * sizeof(uint32_t);
+    PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, gb, hipMemcpyDeviceToHost, s));
     PSGPU_CHECK(hipStreamSynchronize(s));
     const uint32_t* mineG = m->hostGathered + 8 * m->rank;
     if (mine.ctMPUs && (mineG[1] != mine.ctVertices || mineG[2] != mine.ctTriangles)) {
         // finish() re-ran the polygonization with grown buffers: exchange its totals
         rc = m->group ? psgpu_comm_exchange_group(m, m->group) : psgpu_comm_exchange(m, c);
         if (rc != PSGPU_RET_SUCCESS) return rc;
+        PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, gb, hipMemcpyDeviceToHost, s));
         PSGPU_CHECK(hipStreamSynchronize(s));
     }
     m->pending = false;

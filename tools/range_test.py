@@ -20,7 +20,8 @@ for ranks in [int(x) for x in os.environ.get("SHARES", "1,2,4,8").split(",")]:
         for _ in range(neng):
             p = gpu.Polygonizer(0)
             for opt, env in ((gpu.OPT_VERTEX_BLOCKS_PER_CU, "VB"), (gpu.OPT_FINISH_BLOCKS_PER_CU, "FB"),
-                             (gpu.OPT_FINISH_QUAD, "FQ"), (gpu.OPT_BOUND, "BD")):
+                             (gpu.OPT_FINISH_QUAD, "FQ"), (gpu.OPT_BOUND, "BD"),
+                             (gpu.OPT_DEBUG, "DBG"), (gpu.OPT_GRAPH, "GR")):
                 if os.environ.get(env):
                     p.set_option(opt, int(os.environ[env]))
             p.set_model(model)
@@ -38,6 +39,6 @@ for ranks in [int(x) for x in os.environ.get("SHARES", "1,2,4,8").split(",")]:
             p.finish()
         dt = (time.perf_counter() - t0) / K * 1e3
         print(f"rank share 1/{ranks} (MPUs {hi - lo}): {neng} engines VB={os.environ.get('VB', '-')} "
-              f"FB={os.environ.get('FB', '-')} FQ={os.environ.get('FQ', '-')} BD={os.environ.get('BD', '-')} {dt:.4f} ms/step", flush=True)
+              f"FB={os.environ.get('FB', '-')} FQ={os.environ.get('FQ', '-')} BD={os.environ.get('BD', '-')} DBG={os.environ.get('DBG', '-')} GR={os.environ.get('GR', '-')} {dt:.4f} ms/step", flush=True)
         for p in ps:
             p.close()
