@@ -59,6 +59,9 @@ FRAC_OVER_NOTE = (" (reference-priced ops / time exceeds the VALU peak: exact cu
                   "than the reference's op-box pruning, so the reference's op count is not this launch's work; "
                   "see valu_issue / the PMC profile for the hardware-side utilisation)")
 METRIC = "Mcells/sec polygonized, 256^3 grid 32-prim BlobTree, at 1/2/4/8 MI355X"
+# other configs are parity / scaling rehearsals, labelled by their own workload
+METRIC_OTHER = "Mcells/sec polygonized, {n}^3 grid {p}-prim BlobTree ({config}), at {g} MI355X"
+NOFMA_PEAK_TOPS = 78.6  # fp32 VALU lane-ops without FMA (-ffp-contract=off): 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz
 
 
 def spawn_ranks(n: int) -> int:
@@ -171,17 +174,48 @@ def cpu_info():
     return model, smt
 
 
-def cpu_baseline(model, cs, n_cells):
-    """The oracle (oracle/psoracle.c, the CPU restatement of the reference: "port") on the
-    host's cores, bounded sample."""
+def host_cores():
+    """Cores this process may run on: the affinity set, capped by a cgroup CPU quota if one
+    is set (threads past the quota are throttled, not parallel); and the figures behind it."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):  # cgroup v2: "<quota> <period>" or "max <period>"
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:  # cgroup v1
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    cores = aff if quota is None else max(1, min(aff, int(-(-quota // 1))))
+    return cores, {"nproc": nproc, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+                   "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(model, cs, n_cells, config):
+    """The oracle (oracle/psoracle.c, the CPU restatement of the reference: "port") on every
+    core this process may use (host_cores), 2 warm-ups, then up to 10 timed runs within a
+    bounded budget."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import psoracle
 
     psoracle.build()
-    threads = int(os.environ.get("PSGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    cores, why = host_cores()
+    threads = int(os.environ.get("PSGPU_CPU_THREADS", cores))
     times = []
-    psoracle.polygonize(model, cs, threads=threads, keep=False)  # warm-up
+    for _ in range(2):  # warm-ups
+        psoracle.polygonize(model, cs, threads=threads, keep=False)
     t_budget = float(os.environ.get("PSGPU_CPU_SECONDS", "12"))
     t_start = time.perf_counter()
     while len(times) < 10 and (time.perf_counter() - t_start) < t_budget:
@@ -191,10 +225,47 @@ def cpu_baseline(model, cs, n_cells):
     med = float(np.median(times))
     cpu_model, smt = cpu_info()
     return {"value": round(n_cells / med / 1e6, 3), "unit": "Mcells/s", "cores": threads, "kind": "port",
-            "sample": f"full C3 256^3 polygonization x{len(times)} (median {med * 1e3:.1f} ms, "
+            "sample": f"full {config} polygonization x{len(times)} after 2 warm-ups (median {med * 1e3:.1f} ms, "
                       f"best {min(times) * 1e3:.1f} ms) by oracle/psoracle.c, the plain-C restatement of the "
-                      f"reference (PS_Polygonizer.cpp; the reference binary is not built here), {threads} threads",
-            "cpu_model": cpu_model, "nproc": os.cpu_count(), "smt_active": smt}
+                      f"reference (PS_Polygonizer.cpp; the reference binary is not built here), {threads} threads = "
+                      f"the cores this process may use (affinity set, capped by the cgroup CPU quota)",
+            "cpu_model": cpu_model, "smt_active": smt, **why}
+
+
+def latency_single(poly, cs, reps=30):
+    """One engine, one polygonization at a time (enqueue + device chain + host sync): what a
+    blocking caller or a frame-at-a-time editor sees.  Median / best over `reps` runs."""
+    poly.run(cs)
+    t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        poly.run(cs)
+        t.append(time.perf_counter() - t0)
+    return round(float(np.median(t)) * 1e3, 4), round(min(t) * 1e3, 4)
+
+
+def blocking_contract(poly, reps=10):
+    """The reference's own blocking contract, PCIe-inclusive, on C2: psgpu_polygonize_mpus =
+    SimdPoly::run -> Polygonize into the caller's PolyMPUs (PS_HighPerformanceRender.cpp:373-376):
+    model upload, polygonization, mesh download and the scatter into the reference-capacity
+    (24,000 x 21.5 KB) PolyMPUs layout.  Median over `reps` calls after 2 warm-ups."""
+    from parsip_amd import soa
+
+    model, cs, n = synth.make_config("C2")
+    out = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
+    for _ in range(2):
+        rc, ct, _ = poly.polygonize_mpus(cs, model, out)
+        assert rc == 1 and ct == gpu.count_mpus(cs, *model.bbox), (rc, ct)
+    t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        poly.polygonize_mpus(cs, model, out)
+        t.append(time.perf_counter() - t0)
+    med = float(np.median(t))
+    return {"config": f"C2: {model.ct_prims}-prim BlobTree, {n}^3 cells, {ct} MPUs", "ms": round(med * 1e3, 3),
+            "best_ms": round(min(t) * 1e3, 3), "mcells_per_s": round(n ** 3 / med / 1e6, 2),
+            "note": "psgpu_polygonize_mpus end to end (SoA upload, 4 kernels, compact-mesh download over PCIe, "
+                    "host scatter into PolyMPUs); never the bench value"}
 
 
 class Engine:
@@ -293,6 +364,8 @@ def main():
     ap.add_argument("--parts", "--streams", type=int, default=1, dest="parts",
                     help="per engine: the range as this many cost-balanced parts on as many streams")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the single-polygonization latency and the blocking C2 Polygonize timing")
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
                     help="0 interpreter, 1 kernels specialised per tree structure, 2 + parameters baked in")
@@ -338,8 +411,7 @@ def main():
         full = poly.finish()
         costs = poly.mpu_costs()
     if strong:
-        bounds = gpu.split_costs(costs, grp.world)
-        begin, end = int(bounds[grp.rank]), int(bounds[grp.rank + 1])
+        begin, end = gpu.rank_range(costs, grp.world, grp.rank)
     else:
         begin, end = 0, n_mpus
         full = None
@@ -480,9 +552,9 @@ def main():
     pe = profile_entry(pmc, dom, args.jit) if prof_ok else None
     tr, tr_src = committed_profile("traffic")
     te = profile_entry(tr, dom, args.jit) if prof_ok else None
-    roof = {"bound": "valu", "pipe": "fp32 VALU (no MFMA: scalar field evaluation; SURVEY.md §8(d))",
-            "kernel": dom, "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
+    lk = {"bound": "valu", "pipe": "fp32 VALU (no MFMA: scalar field evaluation; SURVEY.md §8(d))",
+            "kernel": dom, "achieved": round(achieved, 3), "peak": NOFMA_PEAK_TOPS, "unit": "T op/s",
+            "frac": round(achieved / NOFMA_PEAK_TOPS, 4),
             "traffic": round(te["traffic_bytes"]) if te and "traffic_bytes" in te else None,
             "traffic_source": tr_src if te else None,
             # the bytes the launch must move (k_mpu: its records and counts out, its queue in)
@@ -506,30 +578,69 @@ def main():
                     "culling skips part of those ops, so valu_issue (executed VALU instructions x 2 cycles per "
                     "wave64 on SIMD-32 / launch cycles, PMC pass of this command) is the hardware-side "
                     "utilisation"}
-    roof["kernels_ms"] = {k: {"span": round(kt[k], 4), "hipevent": round(ev_ms.get(k, 0.0), 4),
+    lk["kernels_ms"] = {k: {"span": round(kt[k], 4), "hipevent": round(ev_ms.get(k, 0.0), 4),
                               "isolated": round(solo.get(k, 0.0), 4)} for k in kt}
     if dom in solo:
         solo_evals = dict(launch_evals, k_mpu=512 * solo_fm / solo_n)[dom]
         a_solo = solo_evals * per_eval / (solo[dom] * 1e-3) / 1e12
-        roof["isolated"] = {"kernel_ms": round(solo[dom], 4), "achieved": round(a_solo, 3),
-                            "frac": round(a_solo / VALU_PEAK_TFLOPS, 4),
+        lk["isolated"] = {"kernel_ms": round(solo[dom], 4), "achieved": round(a_solo, 3),
+                            "frac": round(a_solo / NOFMA_PEAK_TOPS, 4),
                             "note": "engine 0 alone on the device (no concurrent engine), same launches"}
-        if a_solo > VALU_PEAK_TFLOPS:
-            roof["isolated"]["frac"] = None
-            roof["isolated"]["note"] += FRAC_OVER_NOTE
-    if achieved > VALU_PEAK_TFLOPS:
-        roof["frac"] = None
-        roof["note"] += ";" + FRAC_OVER_NOTE
+        if a_solo > NOFMA_PEAK_TOPS:
+            lk["isolated"]["frac"] = None
+            lk["isolated"]["note"] += FRAC_OVER_NOTE
+    if achieved > NOFMA_PEAK_TOPS:
+        lk["frac"] = None
+        lk["note"] += ";" + FRAC_OVER_NOTE
     if pe and "SQ_INSTS_VALU" in pe:
-        roof["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (dur * 1e-3 * 2.4e9 * 1024), 4)
+        lk["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (dur * 1e-3 * 2.4e9 * 1024), 4)
         if dom in solo and "isolated" in roof:
-            roof["isolated"]["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (solo[dom] * 1e-3 * 2.4e9 * 1024), 4)
-        roof["valu_source"] = pmc_src
+            lk["isolated"]["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (solo[dom] * 1e-3 * 2.4e9 * 1024), 4)
+        lk["valu_source"] = pmc_src
     if te and "avg_us" in te:
-        roof["rocprof_avg_us"] = te["avg_us"]
+        lk["rocprof_avg_us"] = te["avg_us"]
+    # primary figure: the executed VALU work of a whole step against the device's VALU issue
+    # capacity over ms_per_step (verdict r02): per-step VALU instructions = sum over the
+    # step's kernels of (mean SQ_INSTS_VALU per launch x launches per step) from the
+    # committed PMC pass of this command; one wave64 VALU instruction occupies a SIMD-32 for
+    # 2 cycles, so issue = instr x 2 / (step seconds x 2.4 GHz x 1024 SIMDs), <= 1 by
+    # construction; the same work in lane-ops (instr x 64, inactive lanes included) against the
+    # no-FMA fp32 ceiling (78.6 T op/s; the FMA peak 157.3 TFLOP/s does not apply to
+    # -ffp-contract=off code) is the same fraction.
+    step = None
+    if pmc and prof_ok:
+        ks = {k: v for k, v in pmc.items() if "SQ_INSTS_VALU" in v and "probe" not in k}
+        first = profile_entry(pmc, "k_precheck", args.jit)
+        steps_prof = (first or {}).get("launches")
+        if ks and steps_prof:
+            instr = sum(v["SQ_INSTS_VALU"] * v.get("launches", steps_prof) for v in ks.values()) / steps_prof
+            sec = ms_step * 1e-3
+            issue = instr * 2 / (sec * 2.4e9 * 1024)
+            lane_tops = instr * 64 / sec / 1e12
+            tr_step = None
+            if tr:
+                tr_step = sum(v.get("traffic_bytes", 0.0) for k, v in tr.items() if "probe" not in k)
+            step = {"bound": "valu", "kernel": "whole step (" + ", ".join(sorted(ks)) + ")",
+                    "achieved": round(lane_tops, 3), "peak": NOFMA_PEAK_TOPS, "unit": "T op/s",
+                    "frac": round(lane_tops / NOFMA_PEAK_TOPS, 4), "valu_issue": round(issue, 4),
+                    "traffic": round(tr_step) if tr_step else None,
+                    "traffic_unit": "HBM bytes per step (sum of the kernels' FETCH_SIZE x 2 + WRITE_SIZE)",
+                    "valu_instr_per_step": round(instr),
+                    "source": pmc_src, "traffic_source": tr_src if tr_step else None,
+                    "peaks": {"no_fma_lane_ops_tops": NOFMA_PEAK_TOPS, "fma_tflops": VALU_PEAK_TFLOPS,
+                              "hbm_gbs": HBM_PEAK_GBS},
+                    "note": "executed work per step: sum over the step's kernels of SQ_INSTS_VALU per launch x "
+                            "launches per step (committed PMC pass of this command), x 64 lanes / ms_per_step "
+                            "(inactive lanes counted: an upper bound on lane-ops); frac = that / 78.6 T op/s, the "
+                            "fp32 VALU ceiling without FMA (the code is built with -ffp-contract=off), which "
+                            "equals valu_issue = instr x 2 cycles / (step x 2.4 GHz x 1024 SIMD-32). The "
+                            "reference-priced per-launch figure of the dominant kernel is 'per_launch'"}
+    roof = step if step else dict(lk)
+    roof["per_launch"] = lk
 
     out = {
-        "metric": METRIC,
+        "metric": METRIC if args.config == "C3" else METRIC_OTHER.format(
+            n=N, p=model.ct_prims, config=args.config, g=grp.world),
         "value": round(value, 2),
         "unit": "Mcells/s",
         "n_gpus": grp.world,
@@ -566,8 +677,14 @@ def main():
     }
     if check:
         out["check"] = check
+    if grp.rank == 0 and grp.world == 1 and not args.no_extras:
+        lat = latency_single(engines[0].p if engines[0].p is not None else poly, cs)
+        out["latency_ms_single"] = {"median": lat[0], "best": lat[1],
+                                    "note": "one engine, one polygonization at a time, host-timed "
+                                            "(enqueue + kernel chain + sync): a blocking caller's latency"}
+        out["blocking_polygonize_mpus"] = blocking_contract(poly)
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3)
+        out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3, args.config)
     if grp.rank == 0:
         print(json.dumps(out), flush=True)
     for e in engines:

@@ -241,7 +241,9 @@ int  psgpu_download_spans(psgpu_ctx* ctx, uint64_t* out, uint32_t* runs);
 int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_KERNEL_TIMING 1   /* 1: record hipEvents around every kernel */
 #define PSGPU_OPT_CULLING       2   /* 1: exact per-wave primitive culling (default) */
-#define PSGPU_OPT_DEBUG         9   /* profiling ablations (bit 0: stop after S2); 0 in use */
+#define PSGPU_OPT_DEBUG         9   /* profiling ablations (bit 0: stop after S2); 0 in use;
+                                       bit 20 (test hook): the next finish re-runs the
+                                       polygonization once as if its k_mpu grid fell short */
 #define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU */
 #define PSGPU_OPT_FINISH_BLOCKS_PER_CU 5  /* persistent k_finish grid */
 #define PSGPU_OPT_GRAPH         7   /* 1: replay repeated launch sequences from a hipGraph (off by
@@ -359,8 +361,12 @@ int  psgpu_comm_exchange(psgpu_comm* comm, psgpu_ctx* ctx);
 /* The same for a rank whose range runs as a group of parts on its one device (several
  * streams): their totals are summed on part 0's stream before the all-gather. */
 int  psgpu_comm_exchange_group(psgpu_comm* comm, psgpu_group* g);
-/* Wait; totals over all ranks and, if parts != NULL, nranks entries (rank order). */
+/* Wait; totals over all ranks and, if parts != NULL, nranks entries (rank order).  A
+ * collective: every rank calls it.  If any rank's finish re-ran its polygonization (grown
+ * buffers), the ranks agree on that (all-reduce MAX of a flag) and all exchange again. */
 int  psgpu_comm_result(psgpu_comm* comm, PsMeshInfo* total, PsGroupPart* parts);
+/* 1 if the last psgpu_comm_result needed that second exchange (tests, diagnostics). */
+int  psgpu_comm_reexchanged(psgpu_comm* comm);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -338,6 +338,9 @@ private:
         if (back.isIdentity()) {
             prims_.idxMatrix[cur] = 0;
         } else {
+            // 128 slots with slot 0 the identity: a 128th transformed primitive has no slot
+            // (the reference adapter would write past SOABlobPrimMatrices::matrix)
+            if (primMats_.count >= PSGPU_MAX_TREE_NODES) return kErrPrimOverflow;
             const uint32_t k = primMats_.count;
             prims_.idxMatrix[cur] = (uint8_t)k;
             float row[16];

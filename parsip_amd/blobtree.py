@@ -502,6 +502,8 @@ def linearize_blobtree(root: BlobNode, raw_types: bool = False, triangle_compat:
             P["idxMatrix"][0, cur] = 0
         else:
             k = int(PM["count"][0])
+            if k >= soa.MAX_TREE_NODES:  # 128 slots, slot 0 the identity (the C++ face returns the same)
+                return PS_ERROR_PRIM_OVERFLOW, 0
             P["idxMatrix"][0, cur] = k
             rows = np.concatenate([back.row(0), back.row(1), back.row(2)])
             PM["matrix"][0, k * 12:(k + 1) * 12] = rows

@@ -448,7 +448,10 @@ struct psgpu_comm {
     int nranks = 0, rank = 0, device = 0;
     uint32_t* gathered = nullptr;      // device: nranks x 8 words
     uint32_t* hostGathered = nullptr;  // pinned copy
+    uint32_t* flag = nullptr;          // device: the "some rank re-ran" all-reduce word
+    uint32_t* hostFlag = nullptr;      // pinned
     bool pending = false;
+    bool reexchanged = false;          // the last result needed the second exchange
     psgpu_ctx* ctx = nullptr;          // the context whose run was exchanged
     psgpu_group* group = nullptr;      // or the group whose parts were summed
 };
@@ -483,7 +486,9 @@ int psgpu_comm_create(psgpu_ctx* ctx, const uint8_t id[PSGPU_COMM_ID_BYTES], int
     rc = nccl_fail(ncclCommInitRank(&m->comm, nranks, u, rank), "ncclCommInitRank");
     if (rc == PSGPU_RET_SUCCESS &&
         (hipMalloc(&m->gathered, (size_t)nranks * 8 * sizeof(uint32_t)) != hipSuccess ||
-         hipHostMalloc(&m->hostGathered, (size_t)nranks * 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess))
+         hipHostMalloc(&m->hostGathered, (size_t)nranks * 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+         hipMalloc(&m->flag, sizeof(uint32_t)) != hipSuccess ||
+         hipHostMalloc(&m->hostFlag, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess))
         rc = PSGPU_RET_DEVICE_ERROR;
     if (rc != PSGPU_RET_SUCCESS) {
         psgpu_comm_destroy(m);
@@ -499,6 +504,8 @@ void psgpu_comm_destroy(psgpu_comm* m) {
     if (m->comm) (void)ncclCommDestroy(m->comm);
     if (m->gathered) (void)hipFree(m->gathered);
     if (m->hostGathered) (void)hipHostFree(m->hostGathered);
+    if (m->flag) (void)hipFree(m->flag);
+    if (m->hostFlag) (void)hipHostFree(m->hostFlag);
     delete m;
 }
 
@@ -556,13 +563,18 @@ int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
 }
 
 // After the exchange: every rank's part (MPU range from the gathered counts, bases in
-// rank order) and the totals over all ranks.  Finishes the context; a run that regrew its
-// buffers and re-ran is exchanged again, synchronously.
+// rank order) and the totals over all ranks.  Finishes the context.  finish() re-runs a
+// polygonization whose buffers or k_mpu grid fell short, after its totals were already
+// exchanged; whether any rank did so is itself agreed collectively (an all-reduce MAX of a
+// flag, on every rank), and then EVERY rank exchanges again -- a collective entered by only
+// the ranks that re-ran would block them forever and leave the others with stale counts.
 int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut) {
     if (!m || !m->pending || !m->ctx) return PSGPU_RET_PARAM_ERROR;
     psgpu_ctx* c = m->ctx;
     PsMeshInfo mine;
     int rc = m->group ? psgpu_group_finish(m->group, &mine, nullptr) : psgpu_finish(c, &mine);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    rc = set_device(c);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     hipStream_t s = c->runStream ? c->runStream : c->stream;
     // the gathered totals of the last exchange come to the host only here (not per step:
@@ -571,8 +583,14 @@ int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut
     PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, gb, hipMemcpyDeviceToHost, s));
     PSGPU_CHECK(hipStreamSynchronize(s));
     const uint32_t* mineG = m->hostGathered + 8 * m->rank;
-    if (mine.ctMPUs && (mineG[1] != mine.ctVertices || mineG[2] != mine.ctTriangles)) {
-        // finish() re-ran the polygonization with grown buffers: exchange its totals
+    *m->hostFlag = (mineG[0] != mine.ctMPUs || mineG[1] != mine.ctVertices || mineG[2] != mine.ctTriangles) ? 1u : 0u;
+    PSGPU_CHECK(hipMemcpyAsync(m->flag, m->hostFlag, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    rc = nccl_fail(ncclAllReduce(m->flag, m->flag, 1, ncclUint32, ncclMax, m->comm, s), "ncclAllReduce");
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    PSGPU_CHECK(hipMemcpyAsync(m->hostFlag, m->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PSGPU_CHECK(hipStreamSynchronize(s));
+    m->reexchanged = *m->hostFlag != 0u;
+    if (m->reexchanged) {  // some rank's totals changed after the exchange: all ranks exchange again
         rc = m->group ? psgpu_comm_exchange_group(m, m->group) : psgpu_comm_exchange(m, c);
         if (rc != PSGPU_RET_SUCCESS) return rc;
         PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, gb, hipMemcpyDeviceToHost, s));
@@ -620,5 +638,7 @@ int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut
     if (totalOut) *totalOut = T;
     return PSGPU_RET_SUCCESS;
 }
+
+int psgpu_comm_reexchanged(psgpu_comm* m) { return (m && m->reexchanged) ? 1 : 0; }
 
 }  // extern "C"

@@ -575,6 +575,9 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     if (c->mpuCount == 0) {  // nothing to launch: an empty result
         memset(c->hostCtr, 0, sizeof(DevCounters));
         c->hostCtr->firstOverflow = 0x7fffffff;
+        // the totals the count exchange reads (k_finish writes them on a real run): zero
+        // MPUs, no overflow -- never a previous run's
+        PSGPU_CHECK(hipMemcpyAsync(c->totals, c->emptyTotals, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         return PSGPU_RET_SUCCESS;
     }
     const Params p = make_params(c);
@@ -843,7 +846,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
         hipMemcpy(c->dTables, &tabHost, sizeof(CubeTablesDev), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&c->dModel, sizeof(DevModel)) != hipSuccess ||
         hipMalloc(&c->ctr, 2 * sizeof(DevCounters)) != hipSuccess ||
-        hipMalloc(&c->totals, 8 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->totals, 16 * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->scanStatus, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
         hipMemset(c->scanStatus, 0, 2 * kScanMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&c->hostCtr, sizeof(DevCounters), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -855,6 +858,14 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     }
     memset(c->hostCtr, 0, sizeof(DevCounters));
     c->hostCtr->firstOverflow = 0x7fffffff;
+    c->emptyTotals = c->totals + 8;  // {0, 0, 0, 0, 0, 0, no overflow, no error}
+    {
+        const uint32_t empty[16] = {0, 0, 0, 0, 0, 0, 0x7fffffffu, 0, 0, 0, 0, 0, 0, 0, 0x7fffffffu, 0};
+        if (hipMemcpy(c->totals, empty, sizeof(empty), hipMemcpyHostToDevice) != hipSuccess) {
+            psgpu_destroy(c);
+            return PSGPU_RET_DEVICE_ERROR;
+        }
+    }
     {
         DevCounters init[2];
         memset(init, 0, sizeof(init));
@@ -999,8 +1010,18 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     const uint64_t total = (uint64_t)c->dims[0] * c->dims[1] * c->dims[2];
     if (total > 0xffffffffull) return PSGPU_RET_PARAM_ERROR;
     const uint32_t end = (uint32_t)std::min<uint64_t>(mpuEnd, total);
-    c->mpuBegin = std::min(mpuBegin, end);
-    c->mpuCount = end - c->mpuBegin;
+    const uint32_t begin = std::min(mpuBegin, end);
+    if (begin != c->mpuBegin || end - begin != c->mpuCount || cellsize != c->lastCs) {
+        // another range or lattice: the last run's survivor count says nothing about this
+        // one -- size k_mpu for the whole range (no re-run) until a run of it finishes.  A new
+        // model on the same lattice (an animation frame) keeps the prediction; a frame that
+        // queues more is re-run by finish(), and psgpu_comm_result agrees on that collectively.
+        c->haveQueued = false;
+        c->lastV = 0;
+    }
+    c->lastCs = cellsize;
+    c->mpuBegin = begin;
+    c->mpuCount = end - begin;
     jit_poll(c, false);
     // capacity from the largest finished run + 1/4 (grows only; finish() still re-runs
     // on an overflow, so a prediction that falls short costs time, never output)
@@ -1036,7 +1057,11 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
                 mv = std::max(mv, h.shard[k].v);
                 mt = std::max(mt, h.shard[k].t);
             }
-            const bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
+            bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
+            if (c->debug & (1 << 20)) {  // test hook: re-run once, as if the grid fell short
+                c->debug &= ~(1 << 20);
+                gridShort = c->mpuCount > 0;
+            }
             c->lastQueued = Q;
             c->lastV = V;
             c->haveQueued = c->mpuCount > 0;

@@ -61,7 +61,8 @@ struct psgpu_ctx {
     size_t capPqMask = 0;
     uint32_t pShardCap = 0;
     uint32_t lastQueued = 0;        // S1 survivors queued for S2 in the last finished run
-    bool haveQueued = false;
+    bool haveQueued = false;        // lastQueued describes the current range and lattice
+    float lastCs = 0.0f;            // the cell size of the last enqueued run
     uint32_t runMpuBlocks = 0;      // k_mpu grid of the last enqueued run
     uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
     uint32_t parity = 0;            // which counter / status set the next run uses
@@ -80,7 +81,8 @@ struct psgpu_ctx {
     float* col = nullptr;
     uint32_t* tris = nullptr;
     DevCounters* ctr = nullptr;         // two sets, alternating runs
-    uint32_t* totals = nullptr;         // 8 words of the last run's totals (k_finish), for RCCL
+    uint32_t* totals = nullptr;         // 8 words of the last run's totals (k_finish), for RCCL,
+    uint32_t* emptyTotals = nullptr;    // then 8 words of an empty run's (totals + 8)
     uint64_t* stamps = nullptr;         // per-wave timeline (PSGPU_OPT_STAMPS), 4 x stampCap x 3 words
     uint32_t stampCap = 0;
     uint64_t* spans = nullptr;          // per-run kernel spans (PSGPU_OPT_SPANS): spanCap x 4 x 2 words

@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_group_gather", "psgpu_group_export_polympus", "psgpu_group_polygonize_mpus",
     "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
     "psgpu_comm_result", "psgpu_download_stamps", "psgpu_comm_exchange_group", "psgpu_download_spans",
+    "psgpu_comm_reexchanged",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -143,6 +144,7 @@ def load(build_if_missing: bool = True):
         "psgpu_comm_exchange": ([vp, vp], i32),
         "psgpu_comm_exchange_group": ([vp, vp], i32),
         "psgpu_comm_result": ([vp, ctypes.POINTER(PsMeshInfo), vp], i32),
+        "psgpu_comm_reexchanged": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -204,6 +206,22 @@ def split_costs(costs: np.ndarray, parts: int, begin: int = 0) -> np.ndarray:
     b = np.zeros(parts + 1, np.uint32)
     _check(load().psgpu_split_costs(c.ctypes.data, len(c), parts, begin, b.ctypes.data), "psgpu_split_costs")
     return b
+
+
+def rank_range(costs: np.ndarray, world: int, rank: int) -> tuple[int, int]:
+    """One rank's MPU range [begin, end) of the strong-scaling split (bench.py, one process
+    per GPU): psgpu_split_costs of the same per-MPU costs on every rank, so the ranks agree
+    without communicating."""
+    b = split_costs(costs, world)
+    return int(b[rank]), int(b[rank + 1])
+
+
+def exclusive_bases(per_rank_counts) -> np.ndarray:
+    """(MPU, vertex, triangle) base of each rank's part in the global mesh from the
+    all-gathered (ctMPUs, ctVertices, ctTriangles) per rank, in rank order -- the host form
+    of what psgpu_comm_result derives from the RCCL all-gather."""
+    c = np.asarray(per_rank_counts, np.int64).reshape(len(per_rank_counts), -1)
+    return np.concatenate([np.zeros((1, c.shape[1]), np.int64), np.cumsum(c, axis=0)[:-1]])
 
 
 @dataclass
@@ -319,6 +337,20 @@ class Polygonizer:
                "psgpu_export_polympus")
         return out[:ct.value]
 
+    def polygonize_mpus(self, cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None = None,
+                        stats: np.ndarray | None = None):
+        """psgpu_polygonize_mpus on this context: the reference's blocking Polygonize (model
+        upload, run, download and scatter into the caller's PolyMPUs).  Returns
+        ``(code, ctMPUs, poly_mpus)``."""
+        if poly_mpus is None:
+            poly_mpus = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
+        ct = ctypes.c_uint32()
+        p, m, o = model.ptrs()
+        rc = self._L.psgpu_polygonize_mpus(self._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
+                                           ctypes.byref(ct), None if stats is None else stats.ctypes.data)
+        self.model = model
+        return rc, ct.value, poly_mpus
+
     def device_mesh(self) -> PsMeshDevice:
         d = PsMeshDevice()
         _check(self._L.psgpu_mesh_device(self._ctx, ctypes.byref(d)), "psgpu_mesh_device")
@@ -376,14 +408,7 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
         return soa.RET_PARAM_ERROR, 0, poly_mpus
     if device not in _DEFAULT:
         _DEFAULT[device] = Polygonizer(device)
-    ctx = _DEFAULT[device]
-    if poly_mpus is None:
-        poly_mpus = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
-    ct = ctypes.c_uint32()
-    p, m, o = model.ptrs()
-    rc = ctx._L.psgpu_polygonize_mpus(ctx._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
-                                      ctypes.byref(ct), None if stats is None else stats.ctypes.data)
-    return rc, ct.value, poly_mpus
+    return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats)
 
 
 def _mesh_from_arrays(V, T, N, fill):
@@ -563,6 +588,10 @@ class Comm:
         parts = (PsGroupPart * self.nranks)()
         _check(self._L.psgpu_comm_result(self._c, ctypes.byref(info), parts), "psgpu_comm_result")
         return info, list(parts)
+
+    def reexchanged(self) -> bool:
+        """Whether the last result() needed the second, collectively agreed exchange."""
+        return bool(self._L.psgpu_comm_reexchanged(self._c))
 
 
 @atexit.register

@@ -152,6 +152,27 @@ def test_cpp_linearizer_errors(exe, tmp_path):
     assert code == bt.linearize_blobtree(acc)[0] in (-1, -2)
 
 
+def _transformed_points(n):
+    aff = bt.Affine(scale=(1.1, 1.0, 0.9), translate=(0.01, 0.0, 0.0))
+    nodes = [bt.Point((0.01 * i, 0, 0), transform=aff) for i in range(n)]
+    while len(nodes) > 1:  # balanced binary tree of Blends
+        nodes = [bt.Op(B.OP_BLEND, nodes[i], nodes[i + 1]) if i + 1 < len(nodes) else nodes[i]
+                 for i in range(0, len(nodes), 2)]
+    return nodes[0]
+
+
+def test_cpp_linearizer_matrix_slots(exe, tmp_path):
+    """SOABlobPrimMatrices holds 128 slots, slot 0 the identity: 127 transformed primitives
+    fit, a 128th is PS_ERROR_PRIM_OVERFLOW (-1) from both faces instead of a write past the
+    array."""
+    code, raw = cpp_linearize(exe, _transformed_points(127), tmp_path)
+    pcode, model = bt.linearize_blobtree(_transformed_points(127))
+    assert code == pcode == 0 and int(model.mats["count"][0]) == 128
+    assert raw == py_bytes(model)
+    code, _ = cpp_linearize(exe, _transformed_points(128), tmp_path)
+    assert code == bt.linearize_blobtree(_transformed_points(128))[0] == bt.PS_ERROR_PRIM_OVERFLOW
+
+
 @pytest.mark.gpu
 def test_cpp_simdpoly_run_and_draw_train(exe, tmp_path, oracle):
     """SimdPoly::linearizeBlobTree + run + draw (compiled C++) on the device, against the

@@ -150,6 +150,79 @@ def test_rccl_exchange_single_rank(gpu_poly):
         comm.close()
 
 
+def test_rccl_exchange_after_rerun_single_rank(gpu_poly):
+    """A run that finish() re-runs after its totals were exchanged (test hook: debug bit 20)
+    is exchanged again, and the result carries the re-run's totals."""
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+    comm = gpu.Comm(gpu_poly, gpu.comm_unique_id(), 1, 0)
+    try:
+        gpu_poly.polygonize(cs)
+        comm.exchange()
+        total, _ = comm.result()
+        assert not comm.reexchanged()
+        ref = (total.ctMPUs, total.ctVertices, total.ctTriangles)
+        gpu_poly.set_option(gpu.OPT_DEBUG, 1 << 20)
+        gpu_poly.polygonize(cs)
+        comm.exchange()
+        total, _ = comm.result()
+        assert comm.reexchanged()
+        assert (total.ctMPUs, total.ctVertices, total.ctTriangles) == ref
+    finally:
+        gpu_poly.set_option(gpu.OPT_DEBUG, 0)
+        comm.close()
+
+
+_TWO_RANK = r"""
+import os, sys
+sys.path.insert(0, os.environ["PSGPU_ROOT"])
+rank = int(sys.argv[1])
+from parsip_amd import gpu, synth
+poly = gpu.Polygonizer(rank)
+import torch.distributed as dist
+dist.init_process_group("gloo", rank=rank, world_size=2)
+model, cs, _ = synth.make_config("C2")
+poly.set_model(model)
+poly.run(cs)
+full = poly.finish()
+b = gpu.split_costs(poly.mpu_costs(), 2)
+obj = [gpu.comm_unique_id() if rank == 0 else None]
+dist.broadcast_object_list(obj, src=0)
+comm = gpu.Comm(poly, obj[0], 2, rank)
+if rank == 1:  # only this rank's finish re-runs: both must still agree and exchange again
+    poly.set_option(gpu.OPT_DEBUG, 1 << 20)
+poly.polygonize(cs, int(b[rank]), int(b[rank + 1]))
+comm.exchange()
+total, parts = comm.result()
+assert comm.reexchanged(), rank
+assert (total.ctMPUs, total.ctVertices, total.ctTriangles) == (full.ctMPUs, full.ctVertices, full.ctTriangles)
+comm.close()
+poly.close()
+dist.destroy_process_group()
+print("ok", rank)
+"""
+
+
+def test_rccl_two_ranks_one_rerun(tmp_path):
+    """Two ranks over RCCL where only rank 1's finish re-runs: the re-exchange is agreed
+    collectively, so neither rank blocks and both get the re-run's totals (needs 2 GPUs)."""
+    if gpu.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL ranks on distinct devices)")
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    script = tmp_path / "two_rank.py"
+    script.write_text(_TWO_RANK)
+    env = dict(os.environ, PSGPU_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    procs = [subprocess.Popen([sys.executable, str(script), str(r)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+
+
 def _bench(args, env_extra=None, timeout=300):
     env = dict(os.environ, **(env_extra or {}))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,

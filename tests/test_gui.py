@@ -303,3 +303,27 @@ def test_gpu_run_polygonizer_api(train):
     assert V > 0 and T > 0 and p.countMPUs() == p.statsIntersectedMPUs()
     assert p.statsTotalCellsInIntersectedMPUs() == 343 * p.statsIntersectedMPUs()
     p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["on_then_off", "off_then_on"])
+def test_gpu_cull_toggle_between_set_tree_and_polygonize(order):
+    """PSGUI_OPT_CULL changed after set_tree applies from the next set_tree: the kernels
+    generated with (or without) culling boxes keep the box pointers they were built with, so
+    turning culling off after a culling set_tree never hands them null boxes; bit-exact."""
+    first = order == "on_then_off"
+    p = gui.ParsipOptimized(0, jit=2, cull=first)
+    p.jit_mode = 2
+    try:
+        _, tree = gui.compact_blobtree(random_tree(7, n_prims=10))
+        p.set_tree(tree)
+        assert p.jit_status() == gui.JIT_ACTIVE
+        gpu_opt = p._L.psgpu_gui_set_option(p._g, gui.OPT_CULL, int(not first))
+        assert gpu_opt == 0
+        gm, om = _both(p, tree, 0.06)
+        assert_gui_mesh_equal(gm, om, f"cull toggled {order}")
+        p.set_tree(tree)  # the new setting now applies; still bit-exact
+        gm, om = _both(p, tree, 0.06)
+        assert_gui_mesh_equal(gm, om, f"cull toggled {order}, after set_tree")
+    finally:
+        p.close()

@@ -25,6 +25,7 @@ for k, c in acc.items():
     if "rocclr" in k or "__amd" in k:
         continue
     e = {n: sum(v) / len(v) for n, v in c.items()}
+    e["launches"] = min(len(v) for v in c.values())  # launches in one pass (each counter is in one pass)
     if dur.get(k):
         us = sorted(dur[k])[len(dur[k]) // 2]
         e["median_us_profiled"] = us
