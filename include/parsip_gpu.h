@@ -242,8 +242,8 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_KERNEL_TIMING 1   /* 1: record hipEvents around every kernel */
 #define PSGPU_OPT_CULLING       2   /* 1: exact per-wave primitive culling (default) */
 #define PSGPU_OPT_DEBUG         9   /* profiling ablations (bit 0: stop after S2); 0 in use;
-                                       bit 20 (test hook): the next finish re-runs the
-                                       polygonization once as if its k_mpu grid fell short */
+                                       bit 20 (test hook): the next run's k_mpu grid is one
+                                       block, so finish must re-run it with the full grid */
 #define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU */
 #define PSGPU_OPT_FINISH_BLOCKS_PER_CU 5  /* persistent k_finish grid */
 #define PSGPU_OPT_GRAPH         7   /* 1: replay repeated launch sequences from a hipGraph (off by

@@ -478,6 +478,7 @@ Params make_params(psgpu_ctx* c) {
     const uint32_t want = c->haveQueued ? (c->lastQueued + c->lastQueued / 4 + 256 + kMpusPerBlock - 1) / kMpusPerBlock
                                         : maxBlocks;
     p.mpuBlocks = std::max(1u, std::min(maxBlocks, want));
+    if (c->debug & (1 << 20)) p.mpuBlocks = 1;  // test hook: a k_mpu grid that falls short (finish re-runs)
     p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
     if (p.scanChunks == 0) p.scanChunks = 1;
     p.scanBlocks = (c->mpuCount + kScanItems * p.scanChunks - 1) / (kScanItems * p.scanChunks);
@@ -581,6 +582,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         return PSGPU_RET_SUCCESS;
     }
     const Params p = make_params(c);
+    c->debug &= ~(1 << 20);  // the short-grid test hook applies to one run
     if (p.spans) c->spanNext++;
     c->runMpuBlocks = p.mpuBlocks;
     const uint32_t slot = c->parity;
@@ -1057,11 +1059,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
                 mv = std::max(mv, h.shard[k].v);
                 mt = std::max(mt, h.shard[k].t);
             }
-            bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
-            if (c->debug & (1 << 20)) {  // test hook: re-run once, as if the grid fell short
-                c->debug &= ~(1 << 20);
-                gridShort = c->mpuCount > 0;
-            }
+            const bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
             c->lastQueued = Q;
             c->lastV = V;
             c->haveQueued = c->mpuCount > 0;

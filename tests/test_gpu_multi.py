@@ -151,8 +151,9 @@ def test_rccl_exchange_single_rank(gpu_poly):
 
 
 def test_rccl_exchange_after_rerun_single_rank(gpu_poly):
-    """A run that finish() re-runs after its totals were exchanged (test hook: debug bit 20)
-    is exchanged again, and the result carries the re-run's totals."""
+    """A run whose k_mpu grid fell short (test hook: debug bit 20, one block) exchanges
+    incomplete totals; finish() re-runs it with the full grid, the ranks agree on a second
+    exchange, and the result carries the complete totals."""
     model, cs, _ = synth.make_config("C2")
     gpu_poly.set_model(model)
     comm = gpu.Comm(gpu_poly, gpu.comm_unique_id(), 1, 0)

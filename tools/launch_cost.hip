@@ -100,6 +100,43 @@ int main() {
     } else {
         printf("module launch: tools/_bin/empty.co not loadable\n");
     }
+    // device-side cost of a dependent kernel: a hipGraph of 64 empty kernels in a chain
+    // (the host launches once), timed with events; 1 and 4 graphs on 4 streams at once
+    for (int grid : {1, 2048}) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CHECK(hipStreamBeginCapture(st[0], hipStreamCaptureModeGlobal));
+        for (int i = 0; i < 64; ++i) hipLaunchKernelGGL(k_empty, dim3(grid), dim3(256), 0, st[0], a);
+        CHECK(hipStreamEndCapture(st[0], &g));
+        CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        for (int i = 0; i < 3; ++i) CHECK(hipGraphLaunch(ge, st[0]));
+        CHECK(hipDeviceSynchronize());
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        for (int S : {1, 4}) {
+            CHECK(hipEventRecord(e0, st[0]));
+            for (int s = 1; s < S; ++s) CHECK(hipStreamWaitEvent(st[s], e0, 0));
+            const int reps = 10;
+            for (int r = 0; r < reps; ++r)
+                for (int s = 0; s < S; ++s) CHECK(hipGraphLaunch(ge, st[s]));
+            for (int s = 1; s < S; ++s) {
+                hipEvent_t es;
+                (void)hipEventCreate(&es);
+                CHECK(hipEventRecord(es, st[s]));
+                CHECK(hipStreamWaitEvent(st[0], es, 0));
+            }
+            CHECK(hipEventRecord(e1, st[0]));
+            CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            printf("graph of 64 dependent empty kernels, grid %d, %d streams at once: %.2f us per kernel per stream, "
+                   "%.2f us per kernel overall\n", grid, S, ms * 1e3 / (reps * 64), ms * 1e3 / (reps * 64 * S));
+            fflush(stdout);
+        }
+        (void)hipGraphExecDestroy(ge);
+        (void)hipGraphDestroy(g);
+    }
     // dependent-launch latency: one stream, launch + sync each time
     {
         const int R = 2000;

@@ -32,10 +32,13 @@ def main():
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--json")
     ap.add_argument("--share", type=int, default=1, help="time the first 1/SHARE of the cost split (a rank's range)")
+    ap.add_argument("--debug", type=int, default=0, help="PSGPU_OPT_DEBUG ablation bits")
     a = ap.parse_args()
     model, cs, N = synth.make_config(a.config)
     p = gpu.Polygonizer(0)
     p.set_option(gpu.OPT_JIT, a.jit)
+    if a.debug:
+        p.set_option(gpu.OPT_DEBUG, a.debug)
     p.set_model(model)
     lo, hi = 0, None
     if a.share > 1:
@@ -88,18 +91,26 @@ def main():
 
 
 
-def mpu_phases(config="C3"):
+def _share_range(p, cs, share):
+    if share <= 1:
+        return 0, None
+    b = p.plan_split(cs, share)
+    return int(b[0]), int(b[1])
+
+
+def mpu_phases(config="C3", share=1):
     """k_mpu phase stamps (debug bit 4096): per real wave, the time spent between entry,
     table staging, MPU fetch + cull mask, S2 walk, the inside-bit barrier, pass 1 (+barrier),
     pass 2 (+barrier) and the end (the k_mpu record's end stamp)."""
     model, cs, N = synth.make_config(config)
     p = gpu.Polygonizer(0)
     p.set_model(model)
+    lo, hi = _share_range(p, cs, share)
     for _ in range(3):
-        p.run(cs)
+        p.run(cs, lo, hi)
     p.set_option(gpu.OPT_STAMPS, 1 << 17)
     p.set_option(gpu.OPT_DEBUG, 4096)
-    p.run(cs)
+    p.run(cs, lo, hi)
     S = p.stamps()
     ph = S["mpu_phases"].astype(np.int64)
     rec = S["k_mpu"].astype(np.int64)
@@ -121,17 +132,18 @@ def mpu_phases(config="C3"):
     print(f"  wave entry time: median {np.median(st):.2f} us, p90 {np.percentile(st, 90):.2f}, max {st.max():.2f}")
 
 
-def precheck_phases(config="C3"):
+def precheck_phases(config="C3", share=1):
     """k_precheck phase stamps (debug bit 8192): per wave, entry -> S1 walk done, -> field
     bounds done (waves holding a survivor), -> queue append, -> end (culling masks)."""
     model, cs, N = synth.make_config(config)
     p = gpu.Polygonizer(0)
     p.set_model(model)
+    lo, hi = _share_range(p, cs, share)
     for _ in range(3):
-        p.run(cs)
+        p.run(cs, lo, hi)
     p.set_option(gpu.OPT_STAMPS, 1 << 17)
     p.set_option(gpu.OPT_DEBUG, 8192)
-    p.run(cs)
+    p.run(cs, lo, hi)
     S = p.stamps()
     rec = S["k_precheck"].astype(np.int64)
     n = len(rec)
@@ -168,11 +180,12 @@ def precheck_phases(config="C3"):
 
 
 if __name__ == "__main__":
+    share = int(os.environ.get("SHARE", "1"))
     if "--precheck" in sys.argv:
         sys.argv.remove("--precheck")
-        precheck_phases()
+        precheck_phases(share=share)
         sys.exit(0)
     if "--phases" in sys.argv:
-        mpu_phases()
+        mpu_phases(share=share)
     else:
         main()
