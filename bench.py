@@ -118,12 +118,12 @@ class Group:
         self.dist.broadcast_object_list(obj, src=0)
         return obj[0]
 
-    def allgather(self, vals):
+    def allgather(self, vals, dtype="int64"):
         if not self.dist:
             return [list(vals)]
         import torch
 
-        t = torch.tensor(list(vals), dtype=torch.int64)
+        t = torch.tensor(list(vals), dtype=getattr(torch, dtype))
         out = [torch.zeros_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t)
         return [o.tolist() for o in out]
@@ -295,6 +295,11 @@ class Engine:
         if self.parts > 1:
             self.obj.set_split(gpu.split_costs(costs[begin:end], self.parts, begin))
 
+    def set_range(self, begin, end, costs):
+        self.begin, self.end = begin, end
+        if self.parts > 1:
+            self.obj.set_split(gpu.split_costs(costs[begin:end], self.parts, begin))
+
     def polygonize(self):
         if self.p is not None:
             self.p.polygonize(self.cs, self.begin, self.end)
@@ -363,6 +368,9 @@ def main():
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; at most 32)")
     ap.add_argument("--parts", "--streams", type=int, default=1, dest="parts",
                     help="per engine: the range as this many cost-balanced parts on as many streams")
+    ap.add_argument("--rebalance", type=int, default=2,
+                    help="strong scaling: rebalance the cost split this many times from the ranks' measured step "
+                         "times before the timed steps (gpu.rebalance)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the single-polygonization latency and the blocking C2 Polygonize timing")
@@ -439,6 +447,37 @@ def main():
         else:
             exchange = "gloo all-gather after the timed steps (ranks share one device: RCCL needs distinct GPUs)"
 
+    # measured-time load balancing (strong scaling): every rank times its range, the times
+    # are all-gathered, and every rank derives the same new split (gpu.rebalance); the cost
+    # model underprices surface-heavy regions, which otherwise set the max over ranks
+    split_log = None
+    if strong and args.rebalance > 0:
+        bounds = [int(x) for x in gpu.split_costs(costs, grp.world)]
+        split_log = {"initial": bounds, "rounds": []}
+        comms = [e.comm for e in engines]
+        for e in engines:
+            e.comm = None  # no count exchange during calibration
+        kcal = 40
+        for it in range(args.rebalance):
+            for k in range(2 * neng):
+                engines[k % neng].polygonize()
+            for e in engines:
+                e.finish()
+            grp.barrier()
+            tc = time.perf_counter()
+            for k in range(kcal):
+                engines[k % neng].polygonize()
+            for e in engines:
+                e.finish()
+            mine_t = (time.perf_counter() - tc) / kcal * 1e3
+            times = [t[0] for t in grp.allgather([mine_t], dtype="float64")]
+            bounds = [int(x) for x in gpu.rebalance(costs, bounds, times)]
+            split_log["rounds"].append({"ms_per_step": [round(t, 4) for t in times], "new_bounds": bounds})
+            begin, end = bounds[grp.rank], bounds[grp.rank + 1]
+            for e in engines:
+                e.set_range(begin, end, costs)
+        for e, c in zip(engines, comms):
+            e.comm = c
     for k in range(max(args.warmup, neng)):
         engines[k % neng].polygonize()
     for e in engines:
@@ -594,7 +633,7 @@ def main():
         lk["note"] += ";" + FRAC_OVER_NOTE
     if pe and "SQ_INSTS_VALU" in pe:
         lk["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (dur * 1e-3 * 2.4e9 * 1024), 4)
-        if dom in solo and "isolated" in roof:
+        if dom in solo and "isolated" in lk:
             lk["isolated"]["valu_issue"] = round(pe["SQ_INSTS_VALU"] * 2 / (solo[dom] * 1e-3 * 2.4e9 * 1024), 4)
         lk["valu_source"] = pmc_src
     if te and "avg_us" in te:
@@ -618,8 +657,10 @@ def main():
             issue = instr * 2 / (sec * 2.4e9 * 1024)
             lane_tops = instr * 64 / sec / 1e12
             tr_step = None
-            if tr:
-                tr_step = sum(v.get("traffic_bytes", 0.0) for k, v in tr.items() if "probe" not in k)
+            tfirst = profile_entry(tr, "k_precheck", args.jit) if tr else None
+            if tfirst and tfirst.get("calls"):  # launches per step from the kernel-trace call counts
+                tr_step = sum(v.get("traffic_bytes", 0.0) * v.get("calls", tfirst["calls"]) / tfirst["calls"]
+                              for k, v in tr.items() if "probe" not in k)
             step = {"bound": "valu", "kernel": "whole step (" + ", ".join(sorted(ks)) + ")",
                     "achieved": round(lane_tops, 3), "peak": NOFMA_PEAK_TOPS, "unit": "T op/s",
                     "frac": round(lane_tops / NOFMA_PEAK_TOPS, 4), "valu_issue": round(issue, 4),
@@ -677,6 +718,9 @@ def main():
     }
     if check:
         out["check"] = check
+    if split_log:
+        out["config"]["split"] = dict(split_log, note="cost split (psgpu_split_costs) refined from all-gathered "
+                                      "measured step times before the timed steps (gpu.rebalance)")
     if grp.rank == 0 and grp.world == 1 and not args.no_extras:
         lat = latency_single(engines[0].p if engines[0].p is not None else poly, cs)
         out["latency_ms_single"] = {"median": lat[0], "best": lat[1],

@@ -216,6 +216,27 @@ def rank_range(costs: np.ndarray, world: int, rank: int) -> tuple[int, int]:
     return int(b[rank]), int(b[rank + 1])
 
 
+def rebalance(costs: np.ndarray, bounds, times) -> np.ndarray:
+    """One step of measured-time load balancing of a contiguous split (strong scaling): the
+    per-MPU costs of rank r's range are scaled by that rank's measured time per unit of
+    cost (times[r] / sum of its costs), so regions the cost model underprices (surface-heavy
+    ones) weigh more, and the scaled costs are split again by psgpu_split_costs.  The inputs
+    are the same on every rank (the times are all-gathered), so every rank derives the same
+    new split."""
+    c = np.asarray(costs, np.float64)
+    b = [int(x) for x in bounds]
+    scaled = np.zeros_like(c)
+    for r in range(len(b) - 1):
+        lo, hi = b[r], b[r + 1]
+        tot = c[lo:hi].sum()
+        if hi > lo and tot > 0:
+            scaled[lo:hi] = c[lo:hi] * (float(times[r]) / tot)
+    if scaled.sum() <= 0:
+        return np.asarray(b, np.uint32)
+    q = np.rint(scaled / scaled.max() * 4.0e6).astype(np.uint32)  # fixed point for the integer split
+    return split_costs(np.maximum(q, 1).astype(np.uint32) if len(q) else q, len(b) - 1, b[0])
+
+
 def exclusive_bases(per_rank_counts) -> np.ndarray:
     """(MPU, vertex, triangle) base of each rank's part in the global mesh from the
     all-gathered (ctMPUs, ctVertices, ctTriangles) per rank, in rank order -- the host form

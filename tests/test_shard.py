@@ -103,3 +103,23 @@ def test_gloo_two_ranks_reassemble(oracle):
     np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), full.stats)
     np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]).view(np.uint32), full.pos.view(np.uint32))
     np.testing.assert_array_equal(np.concatenate([p[2] for p in parts]), full.global_tris())
+
+
+def test_rebalance_moves_work_off_the_slow_rank():
+    """gpu.rebalance (bench.py's measured-time balancing): a rank that measured slower than its
+    cost share gets a smaller range; equal times keep the split; the ranges stay a contiguous
+    cover in order."""
+    rng = np.random.default_rng(1)
+    c = rng.integers(8, 600, size=20000).astype(np.uint32)
+    b = gpu.split_costs(c, 4)
+    same = gpu.rebalance(c, b, [1.0, 1.0, 1.0, 1.0])
+    assert np.all(np.abs(same.astype(np.int64) - b.astype(np.int64)) <= 2)
+    nb = gpu.rebalance(c, b, [1.0, 2.0, 1.0, 1.0])  # rank 1 took twice as long
+    assert nb[0] == 0 and nb[-1] == len(c) and np.all(np.diff(nb.astype(np.int64)) >= 0)
+    assert nb[2] - nb[1] < b[2] - b[1]
+    # predicted times under the measured rates are now closer to equal
+    rate = np.zeros(len(c))
+    for r, t in enumerate([1.0, 2.0, 1.0, 1.0]):
+        rate[b[r]:b[r + 1]] = t / c[b[r]:b[r + 1]].sum()
+    pred = [float((c[nb[r]:nb[r + 1]] * rate[nb[r]:nb[r + 1]]).sum()) for r in range(4)]
+    assert max(pred) / min(pred) < 1.05

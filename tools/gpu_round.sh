@@ -7,7 +7,7 @@
 #   bash tools/gpu_round.sh TAG --collect
 # to copy the summaries into profiles/.
 set -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r03}
 OUT=gpurun_out/$TAG
 if [ "$2" = "--collect" ]; then
   for f in kernel_stats.csv traffic.json pmc.json bench.json bench_c5.json gui_bench.jsonl gui_kernel_stats.csv; do
@@ -26,9 +26,9 @@ if [ "$2" != "notests" ]; then
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
   cat $OUT/smoke.log
 fi
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --no-cpu > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --no-cpu --no-extras > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu --no-extras --steps 5 --warmup 1 > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu --no-extras --steps 5 --warmup 1 > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
 python3 tools/traffic.py $OUT > $OUT/traffic.json && cp $OUT/traffic.json profiles/${TAG}_traffic.json || exit 1
 bash tools/pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
 cp $OUT/pmc/pmc.json profiles/${TAG}_pmc.json || exit 1
@@ -38,7 +38,7 @@ cat $OUT/traffic.json
 timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cp $OUT/bench.json profiles/${TAG}_bench.json
 cat $OUT/bench.json
-timeout -k 10 300 python3 bench.py --config C5 --no-cpu --steps 200 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -20 $OUT/bench_c5.err; exit 1; }
+timeout -k 10 300 python3 bench.py --config C5 --no-cpu --no-extras --steps 200 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -20 $OUT/bench_c5.err; exit 1; }
 cat $OUT/bench_c5.json
 # compat mode (the GUI path): the train scene at three cell sizes, generated kernels, and its
 # kernel trace at cellsize 0.03
