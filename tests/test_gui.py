@@ -318,8 +318,7 @@ def test_gpu_cull_toggle_between_set_tree_and_polygonize(order):
         _, tree = gui.compact_blobtree(random_tree(7, n_prims=10))
         p.set_tree(tree)
         assert p.jit_status() == gui.JIT_ACTIVE
-        gpu_opt = p._L.psgpu_gui_set_option(p._g, gui.OPT_CULL, int(not first))
-        assert gpu_opt == 0
+        assert p._L.psgpu_gui_set_option(p._g, gui.OPT_CULL, int(not first)) == 1  # PSGPU_RET_SUCCESS
         gm, om = _both(p, tree, 0.06)
         assert_gui_mesh_equal(gm, om, f"cull toggled {order}")
         p.set_tree(tree)  # the new setting now applies; still bit-exact
