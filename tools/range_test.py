@@ -7,6 +7,9 @@ import os
 import sys
 import time
 
+# as bench.py: every engine on a hardware queue of its own (the box's default is 4, and a
+# context sharing the null stream's queue slows every step); set before HIP starts
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from parsip_amd import gpu, synth  # noqa: E402
 
@@ -18,7 +21,7 @@ plan.run(cs)
 costs = plan.mpu_costs()
 OPTS = ((gpu.OPT_VERTEX_BLOCKS_PER_CU, "VB"), (gpu.OPT_FINISH_BLOCKS_PER_CU, "FB"), (gpu.OPT_FINISH_QUAD, "FQ"),
         (gpu.OPT_BOUND, "BD"), (gpu.OPT_DEBUG, "DBG"), (gpu.OPT_GRAPH, "GR"))
-TAG = " ".join(f"{e}={os.environ.get(e, '-')}" for _, e in OPTS)
+TAG = " ".join(f"{e}={os.environ.get(e, '-')}" for _, e in OPTS) + f" q={os.environ['GPU_MAX_HW_QUEUES']}"
 
 
 def measure(lo, hi, neng, K):
