@@ -289,6 +289,7 @@ class Engine:
             if args.no_cull:
                 self.obj.set_option(gpu.OPT_CULLING, 0)
             self.obj.set_option(gpu.OPT_JIT, args.jit)
+            self.obj.set_option(gpu.OPT_TREE_SPLIT, args.tree_split)
             if args.debug:
                 self.obj.set_option(gpu.OPT_DEBUG, args.debug)
             self.obj.set_model(model)
@@ -377,6 +378,10 @@ def main():
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=1, choices=[0, 1, 2],
                     help="0 interpreter, 1 kernels specialised per tree structure, 2 + parameters baked in")
+    ap.add_argument("--tree-split", type=int, default=None, choices=[0, 1, 2],
+                    help="OPT_TREE_SPLIT: 1 walk the root's two subtrees in two waves per brick / MPU, 2 only on "
+                         "launches that queue few MPUs (default: 2 for strong scaling over N > 1 ranks, whose "
+                         "shares are small, else 0)")
     ap.add_argument("--debug", type=int, default=0, help=argparse.SUPPRESS)  # profiling ablations only
     args = ap.parse_args()
 
@@ -386,6 +391,8 @@ def main():
     if grp.world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={grp.world}: launch one process per GPU")
     scaling = args.scaling or ("strong" if grp.world > 1 else "weak")
+    if args.tree_split is None:
+        args.tree_split = 2 if scaling == "strong" and grp.world > 1 else 0
 
     # one process per GPU (LOCAL_RANK); PSGPU_BENCH_DEVICE pins every rank to one device
     # (multi-rank rehearsal on a one-GPU box: the count exchange then runs over gloo)
@@ -396,6 +403,7 @@ def main():
     if args.no_cull:
         poly.set_option(gpu.OPT_CULLING, 0)
     poly.set_option(gpu.OPT_JIT, args.jit)
+    poly.set_option(gpu.OPT_TREE_SPLIT, args.tree_split)
     if args.debug:
         poly.set_option(gpu.OPT_DEBUG, args.debug)
 
@@ -704,7 +712,7 @@ def main():
                    "step": "one complete polygonization of the rank's MPU range (all four kernels); steps "
                            "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
-                   "exchange": exchange, "culling": not args.no_cull,
+                   "exchange": exchange, "culling": not args.no_cull, "tree_split": args.tree_split,
                    "kernels": ["interpreter", "jit-structure", "jit-baked"][args.jit] if jit_on or args.jit == 0
                    else "interpreter (jit unavailable)", "set_model_s": round(t_model, 4),
                    "jit_ready_s": round(t_jit, 3)},

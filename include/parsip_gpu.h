@@ -264,6 +264,19 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        wave), 2 (default) the fewest vertices per wave whose waves
                                        hold the last run's vertices in one pass of the persistent
                                        grid (16 or 32; else 64: small rank shares); identical output */
+#define PSGPU_OPT_VERTEX_WIDE  15   /* k_vertex layout: 0 a quad of lanes per vertex (16 per wave),
+                                       1 one lane per vertex walking its 4 edge samples (64 per wave,
+                                       specialised kernels only), 2 (default) 64 when the last run's
+                                       vertices overfill one pass of the persistent grid at 16 per
+                                       wave, else 16; identical output */
+#define PSGPU_OPT_TREE_SPLIT   16   /* 1: k_precheck and k_mpu walk the root's two subtrees in two
+                                       waves per brick / MPU and combine them (specialised kernels,
+                                       trees whose root is a binary op over two ops); 2: only for runs
+                                       whose range queued at most PSGPU_OPT_SPLIT_MAX_QUEUED MPUs for
+                                       S2 last time (small rank shares); 0 (default) one wave walks the
+                                       whole tree.  Non-zero compiles the split kernels too (+30-45 %
+                                       hiprtc time).  Identical output */
+#define PSGPU_OPT_SPLIT_MAX_QUEUED 17  /* threshold of PSGPU_OPT_TREE_SPLIT 2 (default 4 per CU) */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the
                                        specialised kernels on a host thread while the interpreter
                                        serves polygonizations (bit-identical output); 0: block */

@@ -129,6 +129,67 @@ struct BakedOp {
     float lo[3], hi[3], resY;
 };
 
+// Parameter groups of the generated walk (psgpu_jit.cpp, mode 1): the parameters a subtree's
+// walk reads, loaded into SGPRs together at the subtree's entry, so the wave waits for its
+// scalar loads once per group instead of once per primitive (every wait is lgkmcnt(0):
+// scalar loads return out of order).  The empty asm statements pin each value in an SGPR
+// there, so the loads are not sunk back to their first use.
+template <int TYPE>
+__device__ __forceinline__ constexpr bool prim_uses_dir() {
+    return TYPE == PSGPU_T_LINE || TYPE == PSGPU_T_CYLINDER || TYPE == PSGPU_T_DISC || TYPE == PSGPU_T_RING;
+}
+template <int TYPE>
+__device__ __forceinline__ constexpr int prim_res_count() {
+    return TYPE == PSGPU_T_CYLINDER ? 2 : ((TYPE == PSGPU_T_CUBE || TYPE == PSGPU_T_DISC || TYPE == PSGPU_T_RING) ? 1 : 0);
+}
+template <int TYPE>
+__device__ __forceinline__ constexpr bool prim_uses_pos() {
+    return TYPE == PSGPU_T_POINT || TYPE == PSGPU_T_LINE || TYPE == PSGPU_T_CYLINDER || TYPE == PSGPU_T_CUBE ||
+           TYPE == PSGPU_T_DISC || TYPE == PSGPU_T_RING;
+}
+#define PSGPU_PIN(v) asm volatile("" ::"s"(v))
+template <int TYPE, bool MAT>
+__device__ __forceinline__ void load_prim(CPrim& S, BakedPrim& r) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (prim_uses_pos<TYPE>()) r.pos[k] = S.pos[k];
+        if (prim_uses_dir<TYPE>()) r.dir[k] = S.dir[k];
+        if (k < prim_res_count<TYPE>()) r.res[k] = S.res[k];
+    }
+    if (MAT) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) r.mat[k] = S.mat[k];
+    }
+}
+template <int TYPE, bool MAT>
+__device__ __forceinline__ void pin_prim(const BakedPrim& r) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (prim_uses_pos<TYPE>()) PSGPU_PIN(r.pos[k]);
+        if (prim_uses_dir<TYPE>()) PSGPU_PIN(r.dir[k]);
+        if (k < prim_res_count<TYPE>()) PSGPU_PIN(r.res[k]);
+    }
+    if (MAT) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) PSGPU_PIN(r.mat[k]);
+    }
+}
+template <class OP>
+__device__ __forceinline__ void load_op(OP& S, BakedOp& r) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = S.lo[k];
+        r.hi[k] = S.hi[k];
+    }
+}
+__device__ __forceinline__ void pin_op(const BakedOp& r) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        PSGPU_PIN(r.lo[k]);
+        PSGPU_PIN(r.hi[k]);
+    }
+}
+
 template <int TYPE, class PR>
 __device__ __forceinline__ float prim_dist2(PR& P, float x, float y, float z) {
     float d2 = 0.0f;
@@ -579,6 +640,7 @@ struct InterpEval {
     template <int GROUP, bool COLOR, int N>
     __device__ __forceinline__ void evaln(const float* px, const float* py, const float* pz, const CullMask& cm,
                                           float* out, float* colOut) const {
+        static_assert(GROUP != 0, "the interpreter prunes per lane group, not per lane's points");
         for (int n = 0; n < N; ++n)
             out[n] = eval<GROUP, COLOR>(px[n], py[n], pz[n], cm, COLOR ? colOut + 3 * n : nullptr);
     }
@@ -671,15 +733,22 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wav
 // queue pq (one atomic per wave; waves [s*K, (s+1)*K) with K = pShardCap / 8 append to
 // shard s, so a shard cannot overflow).  k_mpu takes them in any order: the mesh order
 // comes from the scan of the per-MPU counts (in k_vertex).
-template <class EV>
+// SPLIT 2 (tree split, TreeEval::kSplit): two waves per brick, one per subtree of the root
+// (evaln_part / bound_part), their values exchanged through LDS and combined by both
+// (combine / bound_combine): the same values, half the walk per wave -- for launches whose
+// span is the heaviest brick's walk (small rank shares, a single engine).  Every wave of the
+// block reaches both barriers; the second wave of a brick stops after them.
+template <class EV, int SPLIT = 1>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
+    const int part = wave % SPLIT;  // subtree of the root this wave walks (SPLIT 2)
+    const int slot = wave / SPLIT;  // the block's brick
     phase_stamp(p, 0, 8192u);
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
     CullLanes cl;  // loaded first: independent of everything below
     if (p.cull) cl = load_cull_lanes(as_const(p.model));
-    const uint32_t W = blockIdx.x * 4u + (uint32_t)wave;  // wave slot: decides the queue shard
+    const uint32_t W = blockIdx.x * (4u / SPLIT) + (uint32_t)slot;  // brick slot: decides the queue shard
     const uint32_t bzN = p.brickDims[2], byN = p.brickDims[1];
     const uint32_t nBricks = p.brickDims[0] * byN * bzN;
     const uint32_t B = W < nBricks ? (uint32_t)(((uint64_t)W * p.brickStride) % nBricks) : W;  // its brick
@@ -700,7 +769,19 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const float pz = Z * p.side + o[2];
     float f = -1.0f;
     CullMask cm{0ull, 0ull};
-    if (!(p.debug & 8u)) {  // ablation bit 3: S1 without the walk (nothing passes)
+    if constexpr (SPLIT == 2) {
+        __shared__ float sF[4][64];
+        cm = cull_mask_points(cl, px, py, pz, p.cull != 0);
+        float fp = -1.0f;
+        if (!(p.debug & 8u)) {
+            if (part == 0) ev.template evaln_part<4, false, 1, 0>(&px, &py, &pz, cm, &fp, nullptr);
+            else ev.template evaln_part<4, false, 1, 1>(&px, &py, &pz, cm, &fp, nullptr);
+        }
+        sF[wave][lane] = fp;
+        __syncthreads();
+        const float rv = sF[slot * 2][lane], lv = sF[slot * 2 + 1][lane];
+        if (!(p.debug & 8u)) ev.template combine<false, 1>(&rv, nullptr, &lv, nullptr, cm, &f, nullptr);
+    } else if (!(p.debug & 8u)) {  // ablation bit 3: S1 without the walk (nothing passes)
         cm = cull_mask_points(cl, px, py, pz, p.cull != 0);
         f = ev.template eval<4, false>(px, py, pz, cm, nullptr);
     } else if (p.debug & 16u) {  // bit 4: the culling mask only
@@ -723,7 +804,46 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     // is exactly one S2 quad); the wave's culling box covers every MPU of the brick.
     uint32_t proven8 = 0;
     if ((p.debug & 1024u) && flags8 != 0u) __builtin_amdgcn_s_setprio(2);  // experiment: heavy waves first
-    if (p.bound && flags8 != 0u) {
+    if constexpr (SPLIT == 2) {
+        __shared__ float sLo[4][64], sHi[4][64];
+        __shared__ uint32_t sOk[4][64];
+        const bool doBound = p.bound && flags8 != 0u;  // the same for both waves of the brick
+        float lo = 0.0f, hi = 0.0f;
+        bool ok = true;
+        BoundBox B;
+        if (doBound) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                B.xs[i] = o[0] + (float)(4 * (c & 1) + i) * p.cs;
+                B.ys[i] = o[1] + (float)(4 * ((c >> 1) & 1) + i) * p.cs;
+                B.zs[i] = o[2] + (float)(4 * (c >> 2) + i) * p.cs;
+            }
+            const float hx = 0.5f * (B.xs[3] - B.xs[0]), hy = 0.5f * (B.ys[3] - B.ys[0]), hz = 0.5f * (B.zs[3] - B.zs[0]);
+            B.cx = 0.5f * (B.xs[0] + B.xs[3]);
+            B.cy = 0.5f * (B.ys[0] + B.ys[3]);
+            B.cz = 0.5f * (B.zs[0] + B.zs[3]);
+            B.h = __builtin_amdgcn_sqrtf(hx * hx + hy * hy + hz * hz) * 1.0001f + 1e-4f;
+            if (part == 0) ev.template bound_part<0>(B, cm, &lo, &hi, &ok);
+            else ev.template bound_part<1>(B, cm, &lo, &hi, &ok);
+        }
+        sLo[wave][lane] = lo;
+        sHi[wave][lane] = hi;
+        sOk[wave][lane] = ok ? 1u : 0u;
+        __syncthreads();
+        if (part != 0) return;  // the brick's first wave finishes it
+        if (doBound) {
+            const int r = slot * 2, l = slot * 2 + 1;
+            ok = sOk[r][lane] != 0u && sOk[l][lane] != 0u;
+            ev.bound_combine(sLo[r][lane], sHi[r][lane], sLo[l][lane], sHi[l][lane], cm, &lo, &hi);
+            const uint64_t bOut = ballot(ok && hi < 0.5f), bIn = ballot(ok && lo >= 0.5f);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const bool all = ((bOut >> (8 * q)) & 0xffull) == 0xffull || ((bIn >> (8 * q)) & 0xffull) == 0xffull;
+                proven8 |= (all ? 1u : 0u) << q;
+            }
+            proven8 &= flags8;
+        }
+    } else if (p.bound && flags8 != 0u) {
         BoundBox B;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // the S2 coordinates (mpu_body): o + (float)index * cs
@@ -824,8 +944,9 @@ __device__ __forceinline__ int find_cell(const uint16_t* first, uint32_t r) {
 
 // Barrier of the MPU's waves (the whole block when W > 1; LDS ordering within the wave
 // when one wave does it all).
+template <int WPM>
 __device__ __forceinline__ void mpu_sync() {
-    if (kMpuWaves > 1) {
+    if (WPM > 1) {
         __syncthreads();
     } else {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -836,19 +957,24 @@ __device__ __forceinline__ void mpu_sync() {
 // Per-MPU body: W = kMpuWaves wavefronts per MPU that passed S1 (and was not proven
 // empty), 4 wavefronts per block.  Every wave of a block reaches every barrier: waves
 // without an MPU (past the last survivor) or whose MPU has no surface just skip the work.
-template <class EV>
+// SPLIT 2 (tree split): two waves per MPU, each walking one subtree of the root over all
+// 8 x-slices (evaln_part), the values exchanged through LDS and combined by both waves
+// (combine), which then share the record passes as the W > 1 x-slice split does.
+template <class EV, int SPLIT = 1>
 __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, uint32_t* item) {
     *item = 0xffffffffu;
+    constexpr int WPM = SPLIT > 1 ? SPLIT : kMpuWaves;  // waves per MPU
+    constexpr int MPB = 4 / WPM;                         // MPUs per block
     const int wave = threadIdx.x >> 6;
     const int lane = lane_id();
-    const int slot = wave / kMpuWaves;  // the block's MPU this wave works on
-    const int part = wave % kMpuWaves;  // its share: x-slices [part * NX, part * NX + NX)
-    constexpr int NX = 8 / kMpuWaves;
+    const int slot = wave / WPM;  // the block's MPU this wave works on
+    const int part = wave % WPM;  // its share: x-slices [part * NX, part * NX + NX), or a subtree
+    constexpr int NX = SPLIT > 1 ? 8 : 8 / kMpuWaves;
     // MPU d = block * (4 / W) + slot is the d-th queued survivor in shard order (dense over
     // the 64 shard queues: lane s holds shard s's count); the grid is sized by the host
     // from the last finished run, and a run with more survivors than that is re-run by finish()
     phase_stamp(p, 0);
-    const uint32_t d = blockIdx.x * (uint32_t)kMpusPerBlock + (uint32_t)slot;
+    const uint32_t d = blockIdx.x * (uint32_t)MPB + (uint32_t)slot;
     ModelPtr M = as_const(p.model);
     const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
     // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
@@ -864,7 +990,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // a run with more survivors than that is re-run by finish()
     const uint32_t incl = sIncl[lane];
     const uint32_t pcount = sIncl[kShards - 1];
-    if (blockIdx.x * (uint32_t)kMpusPerBlock >= pcount) return;  // whole block past the last survivor
+    if (blockIdx.x * (uint32_t)MPB >= pcount) return;  // whole block past the last survivor
     const bool live = d < pcount;
     uint32_t m = 0, w = 0;
     float o[3] = {0.0f, 0.0f, 0.0f};
@@ -883,7 +1009,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         mpu_origin(p, m, o);
     }
     phase_stamp(p, 1);
-    if (kMpuWaves == 1 && !live) return;
+    if (WPM == 1 && !live) return;
     unsigned char* base = smem + slot * kLdsMpu;
     uint16_t* edgeVid = reinterpret_cast<uint16_t*>(base + kLdsEdge);
     uint8_t* cellCfg = base + kLdsCfg;
@@ -894,6 +1020,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     EV ev(M, reinterpret_cast<float*>(smem + kLdsWaveSlots + wave * p.slotsPerLane * 64 * 4) + lane);
     const float cs = p.cs;
 
+    float fs[NX];
     if (live) {
         // S2 (:550-610): corner (x, y, z) of the 8x8x8 cache, lane = y*8 + z, this wave's
         // NX x-slices per lane; quads = 4 consecutive z
@@ -901,13 +1028,17 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         const float py = o[1] + (float)y * cs;
         const float pz = o[2] + (float)z * cs;
         phase_stamp(p, 2);
-        float pxs[NX], pys[NX], pzs[NX], fs[NX];
+        float pxs[NX], pys[NX], pzs[NX];
 #pragma unroll
         for (int x = 0; x < NX; ++x) {
-            pxs[x] = o[0] + (float)(part * NX + x) * cs;
+            pxs[x] = o[0] + (float)((SPLIT > 1 ? 0 : part * NX) + x) * cs;  // SPLIT: both waves walk all 8
             pys[x] = py;
             pzs[x] = pz;
         }
+        if constexpr (SPLIT > 1) {
+            if (part == 0) ev.template evaln_part<4, false, 8, 0>(pxs, pys, pzs, cm, fs, nullptr);
+            else ev.template evaln_part<4, false, 8, 1>(pxs, pys, pzs, cm, fs, nullptr);
+        } else {
 #if PSGPU_S2_N == 1
         // one walk per x-slice in a runtime loop: the walk's code stays resident in the
         // instruction cache (unrolled copies of a 32-primitive walk do not fit)
@@ -924,20 +1055,49 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
             const uint64_t b = ballot(fs[x] >= 0.5f);
             if (lane == 0) sIns[part * NX + x] = b;
         }
+        }
     }
-    phase_stamp(p, 3);
-    mpu_sync();
-    phase_stamp(p, 4);
     uint64_t ins[8];
     uint32_t inside = 0;
+    if constexpr (SPLIT > 1) {  // the parts' values through LDS; both waves combine all 8 slices
+        __shared__ float sS2[4][8][64];
+        if (live) {
+#pragma unroll
+            for (int x = 0; x < 8; ++x) sS2[wave][x][lane] = fs[x];
+        }
+        phase_stamp(p, 3);
+        __syncthreads();
+        phase_stamp(p, 4);
+        if (live) {
+            float rv[8], lv[8], f8[8];
+#pragma unroll
+            for (int x = 0; x < 8; ++x) {
+                rv[x] = sS2[slot * 2][x][lane];
+                lv[x] = sS2[slot * 2 + 1][x][lane];
+            }
+            ev.template combine<false, 8>(rv, nullptr, lv, nullptr, cm, f8, nullptr);
+#pragma unroll
+            for (int x = 0; x < 8; ++x) {
+                ins[x] = ballot(f8[x] >= 0.5f);
+                inside += __popcll(ins[x]);
+            }
+        } else {
+#pragma unroll
+            for (int x = 0; x < 8; ++x) ins[x] = 0ull;
+        }
+    } else {
+    phase_stamp(p, 3);
+    mpu_sync<WPM>();
+    phase_stamp(p, 4);
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
         ins[x] = live ? sIns[x] : 0ull;
         inside += __popcll(ins[x]);
     }
+    }
     const bool work = live && inside != 0 && inside != 512 && !(p.debug & 1u);
     if (live && !work && part == 0 && lane == 0) p.counts[w] = 0ull;  // no vertices, no triangles
-    if (kMpuWaves == 1 && !work) return;
+    if (WPM == 1 && !work) return;
 
     // S3 pass 1 (:647-691): config per cell (bit c = x*4 + y*2 + z, inside = f >= 0.5),
     // owned sign-changing edges (new vertices) and triangles; wave prefix sums give
@@ -988,7 +1148,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         }
     }
     phase_stamp(p, 5);
-    mpu_sync();
+    mpu_sync<WPM>();
     const bool recs = work && !(p.debug & 2u);  // ablation bit 1: pass 1 only
     const uint32_t shard = d & (kShards - 1);
     VertexKey* vk = p.vk + (size_t)shard * p.vShardCap;
@@ -1000,7 +1160,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // Records are written coalesced.
     if (recs) {
         const uint32_t qv = sQ[0];
-        for (uint32_t b0 = (uint32_t)part * 64u; b0 < V; b0 += 64u * kMpuWaves) {
+        for (uint32_t b0 = (uint32_t)part * 64u; b0 < V; b0 += 64u * WPM) {
             const uint32_t r = b0 + (uint32_t)lane;
             if (r < V) {
                 const int c = find_cell(cellV, r);
@@ -1028,13 +1188,13 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         }
     }
     phase_stamp(p, 6);
-    mpu_sync();
+    mpu_sync<WPM>();
     if (!recs || (p.debug & 4u)) return;  // ablation bit 2: no triangles
 
     // pass 3 (S6, :816-825), one lane per triangle r: its cell (last first-id <= r) and
     // the (r - first)-th triangle of the cell's table row
     const uint32_t qt = sQ[1];
-    for (uint32_t b0 = (uint32_t)part * 64u; b0 < T; b0 += 64u * kMpuWaves) {
+    for (uint32_t b0 = (uint32_t)part * 64u; b0 < T; b0 += 64u * WPM) {
         const uint32_t r = b0 + (uint32_t)lane;
         if (r < T) {
             const int c = find_cell(cellT, r);
@@ -1287,7 +1447,7 @@ __device__ __forceinline__ CullMask cull_mask_mpus(const Params& p, uint32_t w) 
 // Quad pruning: the 4 edge samples e1 + (e2-e1)*(l/3), l = 0..3 (:722-762), then the
 // linear root.  The position goes into the vertex record; k_finish evaluates value,
 // colour and normal there (:764-807) and places the vertex in the mesh.
-template <class EV>
+template <class EV, int VPW = 16>
 __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     constexpr int VN = PSGPU_V_N;
     const int wave = threadIdx.x >> 6;
@@ -1302,8 +1462,64 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     __shared__ uint32_t sCnt[kShards];
     stage_shard_counts(p, 1, sCnt);  // ShardCtr::v
     __syncthreads();
-    const ShardBatches sb(sCnt, p.vShardCap, 16 * VN);
     const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
+if constexpr (VPW == 64) {
+    // one lane per vertex: its 4 edge samples as one 4-point walk whose op-box pruning
+    // groups the lane's 4 points (GROUP 0) as the quad layout groups the quad's lanes, so
+    // every value is the same; packed fp32 and one set of uniform work per 4 samples
+    // (more total throughput, a 4x longer walk per wave: chosen for large runs)
+    const ShardBatches sb(sCnt, p.vShardCap, 64);
+    for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sb.locate(batch, &shard, &first, &count);
+        uint32_t rr = first + (uint32_t)lane;
+        const bool valid = rr < count;
+        if (!valid) rr = first;
+        const size_t rec = (size_t)shard * p.vShardCap + rr;
+        const VertexKey R = p.vk[rec];
+        float o[3];
+        mpu_origin(p, R.w + p.mpuBegin, o);
+        const uint32_t key = R.vidKey >> 16;
+        const int sx = key & 7, sy = (key >> 3) & 7, sz = (key >> 6) & 7, ax = (key >> 9) & 3;
+        const float e1x = o[0] + cs * (float)sx;
+        const float e1y = o[1] + cs * (float)sy;
+        const float e1z = o[2] + cs * (float)sz;
+        const float dX = (ax == 0 ? e1x + cs : e1x) - e1x;
+        const float dY = (ax == 1 ? e1y + cs : e1y) - e1y;
+        const float dZ = (ax == 2 ? e1z + cs : e1z) - e1z;
+        float xs[4], ys[4], zs[4], fs[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const float rs = (float)s2 * third;
+            xs[s2] = e1x + dX * rs;
+            ys[s2] = e1y + dY * rs;
+            zs[s2] = e1z + dZ * rs;
+        }
+        CullMask cm{0ull, 0ull};
+        if (p.cull) cm = cull_mask_mpus(p, R.w);
+        if (p.debug & 256u) {  // ablation bit 8: no phase-A walk
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) fs[s2] = xs[s2];
+        } else {
+            ev.template evaln<0, false, 4>(xs, ys, zs, cm, fs, nullptr);
+        }
+        const bool st0 = fs[0] >= 0.5f;
+        const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
+        const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
+        const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
+        const float ax0 = iv == 1 ? xs[0] : (iv == 2 ? xs[1] : xs[2]);
+        const float ay0 = iv == 1 ? ys[0] : (iv == 2 ? ys[1] : ys[2]);
+        const float az0 = iv == 1 ? zs[0] : (iv == 2 ? zs[1] : zs[2]);
+        const float bx0 = iv == 1 ? xs[1] : (iv == 2 ? xs[2] : xs[3]);
+        const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
+        const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
+        const float scale = (0.5f - fa) / (fb - fa);
+        if (valid)
+            p.vp[rec] = VertexPos{{ax0 + scale * (bx0 - ax0), ay0 + scale * (by0 - ay0), az0 + scale * (bz0 - az0)},
+                                  (scale >= 0.0f && scale <= 1.0f) ? 1.0f : 0.0f};
+    }
+} else {
+    const ShardBatches sb(sCnt, p.vShardCap, 16 * VN);
     for (uint32_t batch = blockIdx.x * (blockDim.x >> 6) + wave; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
         sb.locate(batch, &shard, &first, &count);
@@ -1387,6 +1603,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
             }
         }
     }
+}
 }
 
 // Finish: per vertex fieldValueAndColor's value and colour walk (PS_Polygonizer.cpp:777-778,

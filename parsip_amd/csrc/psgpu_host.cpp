@@ -450,6 +450,14 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     return PSGPU_RET_SUCCESS;
 }
 
+// k_precheck / k_mpu with the walk split at the root (two waves per brick / MPU)
+// (2: when the last finished run of this range queued at most splitMaxQueued MPUs for S2 --
+// a launch too small to fill the device, whose span is its heaviest items' walks)
+bool use_split(const psgpu_ctx* c) {
+    if (!c->jit || !c->jit->precheckS || !c->splittable) return false;
+    return c->treeSplit == 1 || (c->treeSplit == 2 && c->haveQueued && c->lastQueued <= c->splitMaxQueued);
+}
+
 Params make_params(psgpu_ctx* c) {
     Params p;
     memset(&p, 0, sizeof(p));  // padding too: graph replay compares parameter bytes
@@ -467,16 +475,17 @@ Params make_params(psgpu_ctx* c) {
     p.mpuCount = c->mpuCount;
     p.cull = (uint32_t)c->cull;
     brick_layout(c, &p.brickI0, p.brickDims);
-    p.preBlocks = (uint32_t)((brick_count(c) + 3) / 4);
+    const bool split = use_split(c);
+    const uint32_t mpb = split ? 2u : (uint32_t)kMpusPerBlock;  // MPUs (bricks) per block
+    p.preBlocks = (uint32_t)((brick_count(c) + mpb - 1) / mpb);
     p.brickStride = brick_stride((uint32_t)brick_count(c), (c->debug & 16384) != 0);
     p.pq = c->pq;
     p.pqMask = c->pqMask;
     p.pShardCap = c->pShardCap;
     // k_mpu: one wave per queued survivor, as many as the last finished run queued + 1/4
     // (a run that queues more is re-run by finish(): the grid then fits exactly)
-    const uint32_t maxBlocks = (c->mpuCount + kMpusPerBlock - 1) / kMpusPerBlock;
-    const uint32_t want = c->haveQueued ? (c->lastQueued + c->lastQueued / 4 + 256 + kMpusPerBlock - 1) / kMpusPerBlock
-                                        : maxBlocks;
+    const uint32_t maxBlocks = (c->mpuCount + mpb - 1) / mpb;
+    const uint32_t want = c->haveQueued ? (c->lastQueued + c->lastQueued / 4 + 256 + mpb - 1) / mpb : maxBlocks;
     p.mpuBlocks = std::max(1u, std::min(maxBlocks, want));
     if (c->debug & (1 << 20)) p.mpuBlocks = 1;  // test hook: a k_mpu grid that falls short (finish re-runs)
     p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
@@ -536,6 +545,18 @@ int finish_vpw(const psgpu_ctx* c) {
     return 64;
 }
 
+// k_vertex layout for the next run (vertices per wave): one lane per vertex (64: each lane's
+// 4 edge samples as one walk, the least total work) when the last run's vertices, 16 per
+// wave, would take more than one pass of the persistent grid; otherwise a quad of lanes per
+// vertex (16: a quarter of the walk per wave, shorter spans).  The interpreter has the quad
+// layout only.
+int vertex_vpw(const psgpu_ctx* c) {
+    if (!c->jit || c->vertexWide == 0) return 16;
+    if (c->vertexWide == 1) return 64;
+    const uint64_t waves = (uint64_t)c->numCUs * (uint64_t)c->vertexBlocksPerCU * 4u;
+    return (uint64_t)c->lastV > 16u * waves ? 64 : 16;
+}
+
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
@@ -543,15 +564,16 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     const int vpw = finish_vpw(c);
     JitKernels* J = c->jit.get();
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
-    if (J) PSGPU_CHECK(launch_jit(J->precheck, p.preBlocks, 256, 0, s, p));
+    const bool split = use_split(c);
+    if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-    if (J) PSGPU_CHECK(launch_jit(J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
+    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
     const uint32_t gridV = std::max(persistV, p.scanBlocks);
-    if (J) PSGPU_CHECK(launch_jit(J->vertex, gridV, 256, 0, s, p));
+    if (J) PSGPU_CHECK(launch_jit(vertex_vpw(c) == 64 ? J->vertexW : J->vertex, gridV, 256, 0, s, p));
     else PSGPU_CHECK(launch_vertex(p, s, gridV));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
     if (J) PSGPU_CHECK(launch_jit(vpw == 16 ? J->finishQ : (vpw == 32 ? J->finishP : J->finish), persistF, 256, 0, s, p));
@@ -585,6 +607,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     c->debug &= ~(1 << 20);  // the short-grid test hook applies to one run
     if (p.spans) c->spanNext++;
     c->runMpuBlocks = p.mpuBlocks;
+    c->runMpb = use_split(c) ? 2u : (uint32_t)kMpusPerBlock;
     const uint32_t slot = c->parity;
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool timed = c->timing != 0;
@@ -596,8 +619,8 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         return rc;
     }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
-    const uint32_t shape[4] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
-                               (uint32_t)finish_vpw(c)};
+    const uint32_t shape[6] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
+                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c), use_split(c) ? 1u : 0u};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
           memcmp(g.shape, shape, sizeof(shape)) == 0)) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -637,7 +660,7 @@ void jit_poll(psgpu_ctx* c, bool wait) {
     c->jit = jit_load(*code, c->device, &c->jitError);
     if (!c->jit && code->code.size() && c->jitError.find("dropped") != std::string::npos) {
         // the cached object would not load: compile it afresh (bypassing the disk cache)
-        c->jitFut = jit_request(c->model, c->useJit == 2, false);
+        c->jitFut = jit_request(c->model, c->useJit == 2, false, c->treeSplit != 0);
         c->jitPending = true;
         if (wait) jit_poll(c, true);
         return;
@@ -651,7 +674,7 @@ void jit_start(psgpu_ctx* c) {
     c->jitPending = false;
     c->jitFut = JitFuture();
     if (!c->useJit || !c->haveModel) return;
-    c->jitFut = jit_request(c->model, c->useJit == 2);
+    c->jitFut = jit_request(c->model, c->useJit == 2, true, c->treeSplit != 0);
     c->jitPending = true;
     jit_poll(c, !c->jitAsync);
 }
@@ -838,6 +861,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, deviceOrdinal) == hipSuccess && prop.multiProcessorCount > 0)
         c->numCUs = prop.multiProcessorCount;
+    c->splitMaxQueued = 4u * (uint32_t)c->numCUs;
     const CubeTables& T = cube_tables();
     CubeTablesDev tabHost{};
     fill_device_tables(T, tabHost);
@@ -938,6 +962,18 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     else if (option == PSGPU_OPT_VERTEX_BLOCKS_PER_CU && value >= 1 && value <= 32) c->vertexBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_FINISH_BLOCKS_PER_CU && value >= 1 && value <= 32) c->finishBlocksPerCU = (int)value;
     else if (option == PSGPU_OPT_FINISH_QUAD && value >= 0 && value <= 3) c->finishQuad = (int)value;
+    else if (option == PSGPU_OPT_VERTEX_WIDE && value >= 0 && value <= 2) c->vertexWide = (int)value;
+    else if (option == PSGPU_OPT_TREE_SPLIT && value >= 0 && value <= 2) {
+        const bool recompile = value != 0 && c->treeSplit == 0 && c->haveModel && c->splittable &&
+                               !(c->jit && c->jit->precheckS);
+        c->treeSplit = (int)value;
+        if (recompile) {  // the loaded kernels lack the split variants: generate them
+            if (c->pending) (void)hipStreamSynchronize(c->runStream);
+            drop_graphs(c);
+            jit_start(c);
+        }
+    }
+    else if (option == PSGPU_OPT_SPLIT_MAX_QUEUED && value >= 0 && value <= 0xffffffffll) c->splitMaxQueued = (uint32_t)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;
@@ -992,6 +1028,7 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     // (jit_get's cache) and the replay key compares the kernels and every parameter
     c->model = *m;
     delete m;
+    c->splittable = jit_splittable(c->model);
     memcpy(&c->primsHost, prims, sizeof(PsSoaBlobPrims));
     PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
     PSGPU_CHECK(hipStreamSynchronize(c->stream));
@@ -1059,7 +1096,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
                 mv = std::max(mv, h.shard[k].v);
                 mt = std::max(mt, h.shard[k].t);
             }
-            const bool gridShort = c->mpuCount > 0 && Q > (uint32_t)kMpusPerBlock * c->runMpuBlocks;
+            const bool gridShort = c->mpuCount > 0 && Q > c->runMpb * c->runMpuBlocks;
             c->lastQueued = Q;
             c->lastV = V;
             c->haveQueued = c->mpuCount > 0;
@@ -1386,7 +1423,7 @@ int psgpu_jit_wait(psgpu_ctx* c) {
 // Generated specialised source for the current model (NUL-terminated, truncated to cap).
 int psgpu_jit_source(psgpu_ctx* c, char* buf, size_t cap) {
     if (!c || !c->haveModel) return PSGPU_RET_PARAM_ERROR;
-    const std::string s = jit_source(c->model, c->useJit == 2);
+    const std::string s = jit_source(c->model, c->useJit == 2, c->treeSplit != 0);
     if (buf && cap) {
         const size_t n = std::min(cap - 1, s.size());
         memcpy(buf, s.data(), n);

@@ -45,6 +45,12 @@ struct psgpu_ctx {
     int vertexBlocksPerCU = 16;  // persistent k_vertex / k_finish grids (256-thread blocks)
     int finishBlocksPerCU = 8;
     int finishQuad = 2;  // PSGPU_OPT_FINISH_QUAD: 0 one lane, 1 a quad, 3 a pair of lanes per vertex, 2 by the last run's vertex count
+    int treeSplit = 0;   // PSGPU_OPT_TREE_SPLIT: 1 k_precheck / k_mpu walk the root's two subtrees in two waves
+    bool splittable = false;  // the model's walk splits at the root (jit_splittable)
+    uint32_t splitMaxQueued = 1024;  // PSGPU_OPT_SPLIT_MAX_QUEUED: tree split 2 applies up to this many S2 MPUs
+                                     // (psgpu_create: 4 per CU; C3's 1/8 shares queue ~800, 1/4 ~1,600)
+    uint32_t runMpb = 0;      // k_mpu MPUs per block of the last enqueued run
+    int vertexWide = 2;  // PSGPU_OPT_VERTEX_WIDE: 0 a quad, 1 one lane per vertex, 2 by the last run's vertex count
     uint32_t lastV = 0;  // vertices of the last finished run (0: none yet)
     int timing = 0;
     // geometry of the last run
@@ -97,7 +103,7 @@ struct psgpu_ctx {
         hipGraphExec_t exec = nullptr;
         JitKernels* jit = nullptr;
         Params key{};
-        uint32_t shape[4] = {0, 0, 0, 0};
+        uint32_t shape[6] = {0, 0, 0, 0, 0, 0};
     } graphs[2];
     float lastMs[kNumKernels] = {};
     PsMeshInfo info{};

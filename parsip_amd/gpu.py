@@ -77,6 +77,9 @@ OPT_JIT_ASYNC = 11
 OPT_STAMPS = 12
 OPT_SPANS = 13
 OPT_FINISH_QUAD = 14
+OPT_VERTEX_WIDE = 15
+OPT_TREE_SPLIT = 16
+OPT_SPLIT_MAX_QUEUED = 17
 STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
 BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3

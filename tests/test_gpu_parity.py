@@ -19,9 +19,11 @@ from parsip_amd.soa import NodeType
 pytestmark = pytest.mark.gpu
 
 
-def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1, jit=1):
+def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1, jit=1, vwide=2, split=0):
     poly.set_option(gpu.OPT_CULLING, cull)
     poly.set_option(gpu.OPT_JIT, jit)
+    poly.set_option(gpu.OPT_VERTEX_WIDE, vwide)
+    poly.set_option(gpu.OPT_TREE_SPLIT, split)
     poly.set_model(model)
     assert poly.jit_active == bool(jit)
     poly.run(cs, begin, end)
@@ -90,6 +92,55 @@ def test_finish_layouts_golden(gpu_poly, name, jit):
         gpu_poly.set_option(gpu.OPT_JIT, 1)
 
 
+@pytest.mark.parametrize("name", ["C2", "C3"])
+@pytest.mark.parametrize("jit", [0, 1])
+def test_vertex_layouts_golden(gpu_poly, name, jit):
+    """k_vertex a quad of lanes per vertex (OPT_VERTEX_WIDE 0), one lane per vertex walking its
+    4 edge samples (1; the interpreter keeps the quad layout) and the per-run choice (2; the
+    second run sees the first run's vertex count) all reproduce the committed oracle digests."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
+    model, cs, _ = synth.make_config(name)
+    gpu_poly.set_option(gpu.OPT_JIT, jit)
+    gpu_poly.set_model(model)
+    try:
+        for mode in (0, 1, 2, 2):
+            gpu_poly.set_option(gpu.OPT_VERTEX_WIDE, mode)
+            gpu_poly.run(cs)
+            gm, gs = gpu_poly.download(), gpu_poly.stats()
+            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+            assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig, (name, jit, mode)
+    finally:
+        gpu_poly.set_option(gpu.OPT_VERTEX_WIDE, 2)
+        gpu_poly.set_option(gpu.OPT_JIT, 1)
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C5"])
+def test_tree_split_golden(gpu_poly, name):
+    """k_precheck / k_mpu with the walk split at the root (OPT_TREE_SPLIT 1: two waves per brick
+    / MPU, values combined through LDS) reproduce the committed oracle digests, then the
+    unsplit kernels on the same context do again (C5: against the unsplit run)."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    digs = json.load(open(os.path.join(gdir, "oracle_digests.json")))
+    model, cs, _ = synth.make_config(name)
+    gpu_poly.set_model(model)
+    seen = []
+    try:
+        for split in (1, 1, 0):
+            gpu_poly.set_option(gpu.OPT_TREE_SPLIT, split)
+            gpu_poly.jit_wait()  # enabling the split compiles the split kernels
+            assert gpu_poly.jit_active
+            gpu_poly.run(cs)
+            gm, gs = gpu_poly.download(), gpu_poly.stats()
+            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+            seen.append(mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()))
+    finally:
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
+    assert seen[0] == seen[1] == seen[2]
+    if name in digs:
+        assert seen[0] == digs[name]
+
+
 def test_engines_pipelined_c3_golden():
     """The bench's pipelining: 4 contexts take 12 C3 polygonizations in turn, queued without
     host synchronisation (bench.py's timed loop); every context's last mesh equals the
@@ -154,13 +205,23 @@ def test_c3_interpreter_and_jit(gpu_poly, oracle, jit):
     assert_mesh_matches(gm, gs, om)
 
 
+@pytest.mark.parametrize("layout", ["default", "vwide", "split"])
 @pytest.mark.parametrize("seed", range(6))
-def test_random_trees(gpu_poly, oracle, seed):
+def test_random_trees(gpu_poly, oracle, seed, layout):
+    """Random trees (every op type, matrices on odd seeds); "vwide" forces k_vertex's
+    lane-per-vertex layout, whose op-box pruning groups a lane's 4 edge samples; "split" walks
+    the root's two subtrees in two waves in k_precheck / k_mpu (trees whose root is a binary
+    op over two ops; the others run unsplit)."""
     ops = [NodeType.BLEND, NodeType.UNION, NodeType.INTERSECT, NodeType.DIF, NodeType.SMOOTHDIF,
            NodeType.RICCIBLEND, NodeType.WARPTWIST, NodeType.GRADIENTBLEND]
     model = synth.random_model(seed, n_prims=3 + 3 * seed, op_types=ops, matrices=seed % 2 == 1)
     cs = float(np.float32(4.0 / 48))
-    gm, gs, om = run_both(gpu_poly, oracle, model, cs, jit=[1, 2, 0][seed % 3])
+    try:
+        gm, gs, om = run_both(gpu_poly, oracle, model, cs, jit=[1, 2, 0][seed % 3],
+                              vwide=1 if layout == "vwide" else 2, split=1 if layout == "split" else 0)
+    finally:
+        gpu_poly.set_option(gpu.OPT_VERTEX_WIDE, 2)
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
     assert_mesh_matches(gm, gs, om)
 
 

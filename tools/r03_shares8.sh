@@ -10,7 +10,7 @@ CONFIG=C3 SHARES=1,2,4,8 REBAL=2 ENGINES=4 VB=8 FB=4 K=400 timeout -k 10 300 pyt
 grep "slowest\|1/1" $OUT/c3.txt
 CONFIG=C5 SHARES=1,2,4,8 REBAL=2 ENGINES=4 VB=8 FB=4 K=200 timeout -k 10 400 python3 -u tools/range_test.py > $OUT/c5.txt 2>&1 || { tail -5 $OUT/c5.txt; exit 1; }
 grep "slowest\|1/1" $OUT/c5.txt
-GPU_MAX_HW_QUEUES=4 CONFIG=C3 SHARES=8 ENGINES=4 VB=8 FB=4 K=400 timeout -k 10 200 python3 -u tools/range_test.py > $OUT/c3_q4.txt 2>&1 || { tail -5 $OUT/c3_q4.txt; exit 1; }
+RT_QUEUES=4 CONFIG=C3 SHARES=8 ENGINES=4 VB=8 FB=4 K=400 timeout -k 10 200 python3 -u tools/range_test.py > $OUT/c3_q4.txt 2>&1 || { tail -5 $OUT/c3_q4.txt; exit 1; }
 grep "rank 0\|rank 4" $OUT/c3_q4.txt
 # the empty step (every MPU fails S1: launch + kernel-boundary floor) at 8 queues, 1 and 4 engines
 CONFIG=C3 SHARES=8 ENGINES=1,4 VB=8 FB=4 DBG=8 K=400 timeout -k 10 120 python3 -u tools/range_test.py > $OUT/c3_empty.txt 2>&1 || { tail -5 $OUT/c3_empty.txt; exit 1; }

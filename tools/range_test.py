@@ -9,7 +9,7 @@ import time
 
 # as bench.py: every engine on a hardware queue of its own (the box's default is 4, and a
 # context sharing the null stream's queue slows every step); set before HIP starts
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_QUEUES", "8")  # RT_QUEUES=4: the box's default
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from parsip_amd import gpu, synth  # noqa: E402
 
@@ -20,7 +20,7 @@ plan.set_model(model)
 plan.run(cs)
 costs = plan.mpu_costs()
 OPTS = ((gpu.OPT_VERTEX_BLOCKS_PER_CU, "VB"), (gpu.OPT_FINISH_BLOCKS_PER_CU, "FB"), (gpu.OPT_FINISH_QUAD, "FQ"),
-        (gpu.OPT_BOUND, "BD"), (gpu.OPT_DEBUG, "DBG"), (gpu.OPT_GRAPH, "GR"))
+        (gpu.OPT_BOUND, "BD"), (gpu.OPT_DEBUG, "DBG"), (gpu.OPT_GRAPH, "GR"), (gpu.OPT_VERTEX_WIDE, "VW"), (gpu.OPT_JIT, "JIT"), (gpu.OPT_TREE_SPLIT, "TS"), (gpu.OPT_SPLIT_MAX_QUEUED, "SMQ"))
 TAG = " ".join(f"{e}={os.environ.get(e, '-')}" for _, e in OPTS) + f" q={os.environ['GPU_MAX_HW_QUEUES']}"
 
 
@@ -34,7 +34,7 @@ def measure(lo, hi, neng, K):
         p.set_model(model)
         p.run(cs, lo, hi)
         ps.append(p)
-    for k in range(20):
+    for k in range(max(50, K // 4)):  # warm-up (the first range a process times runs slow otherwise)
         ps[k % neng].polygonize(cs, lo, hi)
     for p in ps:
         p.finish()
