@@ -387,6 +387,11 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    # stdout carries exactly one line, the JSON result: anything libraries print there (gloo's
+    # "[Gloo] Rank 0 is connected to ..." at connection time) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     grp = Group()
     if grp.world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={grp.world}: launch one process per GPU")
@@ -738,7 +743,7 @@ def main():
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3, args.config)
     if grp.rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     for e in engines:
         e.close()
     if grp.dist:

@@ -229,8 +229,8 @@ def _bench(args, env_extra=None, timeout=300):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
                        text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = r.stdout.strip().splitlines()  # the contract: stdout is the JSON line and nothing else
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     return json.loads(lines[0])
 
 
