@@ -14,7 +14,7 @@
  * The node classes named here are the reference's (PS::BLOBTREE, PS_BlobTree/include/):
  * CBlobNode (CBlobTree.h:29), CSkeletonPrimitive (CSkeletonPrimitive.h:24), the skeletons
  * CSkeletonPoint/Line/Ring/Disc/Cylinder/Cube/Triangle, CQuadricPoint, and the operators
- * CPcm, CRicciBlend, CWarpTwist, CWarpTaper, CWarpBend, CWarpShear.  It also binds the
+ * CPcm, CRicciBlend, CWarpTwist, CWarpTaper, CWarpBend, CWarpShear, CInstance.  It also binds the
  * compat mode (parsip_gpu_gui.hpp) as PS::CParsipOptimizedGpu.
  */
 #ifndef PARSIP_GPU_BLOBTREE_HPP
@@ -40,6 +40,7 @@ struct ParsipBlobTreeApi {
     typedef PS::BLOBTREE::CWarpBend WarpBend;
     typedef PS::BLOBTREE::CWarpShear WarpShear;
     typedef PS::BLOBTREE::CQuadricPoint QuadricPoint;  // compat mode only (parsip_gpu_gui.hpp)
+    typedef PS::BLOBTREE::CInstance Instance;          // compat mode only
 };
 
 /* class SimdPoly (PS_HighPerformanceRender.h:15-33) on the device. */

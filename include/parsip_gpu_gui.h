@@ -12,7 +12,8 @@
  *     -1/delta central differences (:433-450), colours by baseColor over the field values
  *     stored by the last Newton evaluation (:1095-1294);
  *   - the field: n-ary operators, Ricci blend with powf, per-node backward matrices,
- *     warps (bend, twist, taper, shear), no op-box pruning (:677-1092).
+ *     warps (bend, twist, taper, shear), PCM contact and Instance nodes, no op-box
+ *     pruning (:677-1092).
  * Every entry point below replaces the reference function named beside it.  The tree is
  * passed as the COMPACTBLOBTREE arrays (CompactBlobTree.h:26-61) with the per-operator
  * kid lists flattened into one array.  No CPU fallback: without a device every compute
@@ -37,6 +38,9 @@ extern "C" {
 #define PSGUI_PRIM_TRIANGLE     7
 #define PSGUI_PRIM_QUADRICPOINT 10
 #define PSGUI_PRIM_NULL         12
+#define PSGUI_PRIM_INSTANCE     13   /* res1 = (origin's compact id, origin orgID, origin
+                                        isOp, origin type): CompactBlobTree.cpp:383-391,
+                                        resolved by updateInstanceNodes (:410-431)        */
 #define PSGUI_OP_UNION          14
 #define PSGUI_OP_INTERSECT      15
 #define PSGUI_OP_DIF            16
@@ -52,10 +56,18 @@ extern "C" {
 #define PSGUI_MAX_DEPTH         32   /* operator nesting the device walk supports        */
 #define PSGUI_GRID_DIM          8    /* GRID_DIM (CPolyParsipOptimized.h:23, GRID_DIM_8)  */
 #define PSGUI_ITERATIONS        8    /* DEFAULT_ITERATIONS (_constSettings.h:8)           */
-#define PSGUI_RET_UNSUPPORTED  -7    /* a node the compact walk does not evaluate here:
-                                        Instance, PCM (its contact state is shared mutable
-                                        state, CompactBlobTree.cpp:501-569), an operator
-                                        without children, nesting > PSGUI_MAX_DEPTH       */
+#define PSGUI_RET_UNSUPPORTED  -7    /* a tree the device walk does not evaluate: an operator
+                                        without children, nesting > PSGUI_MAX_DEPTH (an
+                                        Instance's origin subtree counted where the Instance
+                                        sits), a PCM without exactly 2 kids (the reference
+                                        returns 0 and reads an uninitialised kid colour),
+                                        a PCM inside a PCM's kid subtree (also through an
+                                        Instance), an Instance of a subtree holding an
+                                        Instance (nested instancing; this also excludes
+                                        cycles)                                            */
+#define PSGUI_PCM_MARCH_MAX     64   /* marchTowardNode's steps (CompactBlobTree.cpp:572-592
+                                        loops until |f - iso| < 1e-3, forever when it never
+                                        gets there)                                        */
 
 /* BlobPrimitive (CompactBlobTree.h:26-38); vec4f fields as float[4]. */
 typedef struct PsGuiPrim {
@@ -139,14 +151,33 @@ int  psgpu_gui_finish(psgpu_gui* g, PsGuiInfo* info);
 int  psgpu_gui_download(psgpu_gui* g, float* pos, float* nrm, float* col4, uint32_t* tris,
                         uint64_t* mpuOffsets, PsGuiMpuStats* stats);
 
-/* COMPACTBLOBTREE::fieldvalue and baseColor at n points (probe; col4 may be NULL). */
+/* COMPACTBLOBTREE::fieldvalue and baseColor at n points (probe; col4 may be NULL).  PCM
+ * nodes read the contact state below and never update it. */
 int  psgpu_gui_field_values(psgpu_gui* g, const float* xyz, uint32_t n, float* out, float* col4);
+
+/* The PCM contact state (PCMCONTEXT maxCompressionLeft / Right, CompactBlobTree.h:63-71),
+ * one pair per tree shared by its PCM nodes, as the reference's.  The reference keeps it as
+ * a running maximum that each TBB body's copy of the tree updates in its own evaluation
+ * order (CompactBlobTree.cpp:508-521, a copy per body: CPolyParsipOptimized.h:171,188), so
+ * its propagation fields depend on how TBB split the MPU range.  The defined order here:
+ * a polygonization reads the state as it was when the run started (set_tree = convert sets
+ * ISO_VALUE, :82-87: what every body of the reference starts from) and, when it ends,
+ * raises the state to the largest compression any of its field evaluations met (the
+ * corner cache, Newton steps and their gradient samples, normal samples -- exactly the
+ * reference's evaluations).  get reads it (after finish); set replaces it
+ * (stream-ordered, for the next run or probe). */
+int  psgpu_gui_get_pcm_state(psgpu_gui* g, float state[2]);
+int  psgpu_gui_set_pcm_state(psgpu_gui* g, const float state[2]);
 
 /* Per-tree kernels.  set_tree starts compiling the tree's walk as straight-line code
  * (hiprtc, on a host thread; parameters stay in device memory, so only a structural edit
  * recompiles) while the interpreter kernels serve; polygonize swaps them in once loaded.
  * Both are bit-identical.  PSGUI_OPT_JIT: 0 interpreter only, 1 swap in when ready
- * (default; environment PSGUI_JIT overrides), 2 set_tree waits for the compile. */
+ * (default; environment PSGUI_JIT overrides), 2 set_tree waits for the compile.
+ * Trees with PCM or Instance nodes always run the interpreter's extended walk, without
+ * culling (their sub-walks leave the wave's points: PCM marches toward a kid's surface, an
+ * Instance evaluates its origin at its own point); their jit status stays NONE and
+ * psgpu_gui_jit_compile returns PSGUI_RET_UNSUPPORTED for them. */
 #define PSGUI_OPT_JIT           1
 /* PSGUI_OPT_CULL (1 default; environment PSGUI_CULL overrides; takes effect at the next
  * set_tree): skip a primitive, or a whole operator subtree, when no point of the wave lies

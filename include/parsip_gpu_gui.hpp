@@ -15,8 +15,10 @@
  *   psgpu::Run_Polygonizer        Run_Polygonizer (:615-628).
  *
  * `Api` names the caller's classes as for SimdPolyT (parsip_gpu.hpp), plus
- *   Api::Node::getID(), the material's diffuse alpha (diffused.w), and
- *   Api::QuadricPoint with getPosition(), getFieldRadius(), getFieldScale().
+ *   Api::Node::getID(), the material's diffuse alpha (diffused.w),
+ *   Api::QuadricPoint with getPosition(), getFieldRadius(), getFieldScale(), and
+ *   Api::Instance with getOriginalNode().
+ * The PCM contact state: ParsipOptimizedT::pcmState / setPcmState (parsip_gpu_gui.h).
  * parsip_gpu_blobtree.hpp binds it to ParsipHaptics' PS::BLOBTREE classes.
  */
 #ifndef PARSIP_GPU_GUI_HPP
@@ -48,9 +50,19 @@ public:
         ops.clear();
         kids.clear();
         mtx.assign(1, PsGuiMatrix{{{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}}});
+        converted_.clear();
         if (!root) return kErrParamError;
         int isOp = 0;
-        return rec(root, isOp);
+        const int res = rec(root, isOp);
+        // updateInstanceNodes (:410-431): an Instance's origin by its node id
+        for (PsGuiPrim& p : prims)
+            if (p.type == PSGUI_PRIM_INSTANCE && (int)p.res1[0] == -1)
+                for (const auto& c : converted_)
+                    if (c.first == (int)p.res1[1]) {
+                        p.res1[0] = (float)c.second;
+                        break;
+                    }
+        return res;
     }
 
     std::vector<PsGuiPrim> prims;
@@ -59,6 +71,8 @@ public:
     std::vector<PsGuiMatrix> mtx;
 
 private:
+    std::vector<std::pair<int, int>> converted_;  // m_lstConvertedIds: (node id, compact id)
+
     template <class V>
     static void set4(float* d, const V& v, float w = 0.0f) {
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = w;
@@ -135,6 +149,7 @@ private:
             default:
                 return kErrNodeNotRecognized;
             }
+            converted_.push_back({n->getID(), cur});
             return cur;
         }
         const int cur = (int)prims.size();  // :242-401
@@ -205,11 +220,23 @@ private:
         } break;
         case PSGUI_PRIM_NULL:
             break;
+        case PSGUI_PRIM_INSTANCE: {  // :383-391, resolved after the walk
+            Node* o = reinterpret_cast<typename Api::Instance*>(n)->getOriginalNode();
+            if (!o) {
+                prims.push_back(p);
+                return kErrParamError;
+            }
+            p.res1[0] = -1.0f;
+            p.res1[1] = (float)o->getID();
+            p.res1[2] = o->isOperator() ? 1.0f : 0.0f;
+            p.res1[3] = (float)(int)o->getNodeType();
+        } break;
         default:
             prims.push_back(p);
             return kErrNodeNotRecognized;
         }
         prims.push_back(p);
+        converted_.push_back({n->getID(), cur});
         return cur;
     }
 };
@@ -266,6 +293,9 @@ public:
     size_t statsTotalCellInAllMPUs() const { return (size_t)(PSGUI_GRID_DIM - 1) * (PSGUI_GRID_DIM - 1) * (PSGUI_GRID_DIM - 1) * countMPUs(); }
     size_t statsTotalCellsInIntersectedMPUs() const { return (size_t)info_.ctCellsInIntersectedMPUs; }
     const PsGuiInfo& info() const { return info_; }
+    /* the PCM contact state (maxCompressionLeft, Right) the next run reads */
+    int pcmState(float state[2]) { return ok() ? psgpu_gui_get_pcm_state(g_, state) : status_; }
+    int setPcmState(const float state[2]) { return ok() ? psgpu_gui_set_pcm_state(g_, state) : status_; }
     int id() const { return id_; }
     const CompactTreeT<Api>& compactTree() const { return tree_; }
 

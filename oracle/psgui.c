@@ -19,6 +19,15 @@
  * glibc 2.35's powf / cosf / sinf differ from the correctly rounded value by 1 ulp on about
  * 0.4 % / 1 % of arguments (tests/test_gui.py measures it on the scene's own arguments).
  *
+ * PCM (precise contact modelling, CompactBlobTree.cpp:490-614) keeps a contact state, the
+ * PCMCONTEXT maxima, that the reference updates as a running maximum in each TBB body's
+ * copy of the tree, so its propagation fields depend on the body split.  The defined order
+ * restated here (and on the device, include/parsip_gpu_gui.h): a run reads the state it
+ * started with (cur*) and raises the state to the largest compression its evaluations met
+ * when it ends (max*); probes read it and never change it.  marchTowardNode stops after
+ * PSGUI_PCM_MARCH_MAX steps (the reference loops until it converges, forever if it never
+ * does).
+ *
  * Parity status: no output of this path is recorded in the reference beyond
  * Distrib/ParsipHaptics_Release.csv, which came from a different build and scene (see
  * DESIGN.md §6): "parity unpinned" beyond the restatement, the shared MC table digest and
@@ -51,13 +60,23 @@ typedef struct { float x, y, z, w; } v4;
 typedef struct { float x, y, z; } v3;
 
 typedef struct {
+    float curL, curR;  /* maxCompressionLeft / Right as the run started (read)             */
+    float maxL, maxR;  /* the running maxima (written when `update`)                       */
+    int update;
+} PcmCtx;
+
+typedef struct {
     const PsGuiPrim* P;
     uint32_t nP;
     const PsGuiOp* O;
     uint32_t nO;
     const uint32_t* K;
     const PsGuiMatrix* M;
+    PcmCtx* pcm;
 } Tree;
+
+#define ISO_DISTANCE 0.454202f  /* _constSettings.h:11 */
+static float field_op(const Tree* T, v4 p, int id, float* storeOp, float* storePrim);
 
 static float cr_powf(float x, float y) { return (float)pow((double)x, (double)y); }
 static float cr_cosf(float x) { return (float)cos((double)x); }
@@ -285,6 +304,12 @@ static float field_prim(const Tree* T, v4 p, int id, float* storePrim) {
         float f = (1.0f - (d2 / (R * R)));
         fv = (f <= 0.0f) ? 0.0f : P->res2[0] * f * f;
     } break;
+    case PSGUI_PRIM_INSTANCE: {  /* :1069-1078 */
+        int isOriginOp = P->res1[2] != 0.0f;
+        int idxOrigin = (int)P->res1[0];
+        v4 myp = {pn.x, pn.y, pn.z, 1.0f};
+        fv = isOriginOp ? field_op(T, myp, idxOrigin, 0, 0) : field_prim(T, myp, idxOrigin, 0);
+    } break;
     default:  /* Null */
         fv = 0.0f;
         break;
@@ -364,6 +389,110 @@ static v4 warp_shear(v4 pin, float f, int along, int dep) {
     return out;
 }
 
+/* fieldAtNode (:646-652) */
+static float field_at_node(const Tree* T, int isOp, int id, v4 p) {
+    return isOp ? field_op(T, p, id, 0, 0) : field_prim(T, p, id, 0);
+}
+
+/* gradientAtNode (:617-643) */
+static v4 gradient_at_node(const Tree* T, int isOp, int id, v4 p, float fp, float delta) {
+    float inv = 1.0f / delta;
+    v4 a = {p.x + delta, p.y + 0.0f, p.z + 0.0f, p.w + 0.0f};
+    v4 b = {p.x + 0.0f, p.y + delta, p.z + 0.0f, p.w + 0.0f};
+    v4 c = {p.x + 0.0f, p.y + 0.0f, p.z + delta, p.w + 0.0f};
+    v4 res = {field_at_node(T, isOp, id, a), field_at_node(T, isOp, id, b), field_at_node(T, isOp, id, c), 0.0f};
+    res.x -= fp; res.y -= fp; res.z -= fp; res.w -= 0.0f;
+    res.x *= inv; res.y *= inv; res.z *= inv; res.w *= inv;
+    return res;
+}
+
+/* marchTowardNode (:572-592); fp is updated in place */
+static v3 march_toward_node(const Tree* T, int isOp, int id, v3 p, v3 grad, float* fp) {
+    int dir = (*fp < ISO_VALUE) ? 1 : -1;
+    int dir2;
+    float step = ISO_DISTANCE;
+    v3 q = p;
+    for (int it = 0; it < PSGUI_PCM_MARCH_MAX && !(((ISO_VALUE - FIELD_VALUE_EPSILON) < *fp) && (*fp < (ISO_VALUE + FIELD_VALUE_EPSILON)));
+         ++it) {
+        float s = step * (float)dir;
+        q.x += grad.x * s; q.y += grad.y * s; q.z += grad.z * s;
+        v4 q4 = {q.x, q.y, q.z, 0.0f};
+        *fp = field_at_node(T, isOp, id, q4);
+        dir2 = (*fp < ISO_VALUE) ? 1 : -1;
+        if (dir != dir2) step *= 0.5f;
+        dir = dir2;
+    }
+    return q;
+}
+
+/* computePropagationDeformation (:594-614) */
+static float propagation_deformation(float dist, float k, float a0, float w) {
+    float wh = 0.5f * w;
+    float w2 = w * w;
+    float w3 = w2 * w;
+    if (dist >= 0 && dist < wh) {
+        float p1 = (4.0f * (w * k - 4 * a0)) / w3;
+        float p2 = (4.0f * (3.0f * a0 - w * k)) / w2;
+        float d2 = dist * dist;
+        float d3 = dist * d2;
+        return p1 * d3 + p2 * d2 + k * dist;
+    } else if (dist >= wh && dist < w) {
+        return (4 * a0 + (dist - w) * (dist - w) * (4 * dist - w)) / w3;
+    }
+    return 0.0f;
+}
+
+static const float* oct_of(const Tree* T, int isOp, int id, int hi) {
+    return isOp ? (hi ? T->O[id].octHi : T->O[id].octLo) : (hi ? T->P[id].octHi : T->P[id].octLo);
+}
+
+/* computePCM (:490-570) */
+static float compute_pcm(const Tree* T, v4 p, const PsGuiOp* O, int id1, int id2, int isOp1, int isOp2, float fp1,
+                         float fp2) {
+    PcmCtx* C = T->pcm;
+    const float *lo1 = oct_of(T, isOp1, id1, 0), *hi1 = oct_of(T, isOp1, id1, 1);
+    const float *lo2 = oct_of(T, isOp2, id2, 0), *hi2 = oct_of(T, isOp2, id2, 1);
+    int crossed = !((lo1[0] >= hi2[0]) || (hi1[0] <= lo2[0]) || (lo1[1] >= hi2[1]) || (hi1[1] <= lo2[1]) ||
+                    (lo1[2] >= hi2[2]) || (hi1[2] <= lo2[2]));  /* intersects (_GlobalFunctions.h:34-44) */
+    if (crossed) {
+        if (fp1 >= ISO_VALUE && fp2 >= ISO_VALUE) {
+            if (fp1 > fp2) {
+                if (C->update && fp2 > C->maxL) C->maxL = fp2;
+                return fp1 + (ISO_VALUE - fp2);
+            } else {
+                if (C->update && fp1 > C->maxR) C->maxR = fp1;
+                return fp2 + (ISO_VALUE - fp1);
+            }
+        } else if (fp1 >= ISO_VALUE && fp2 > FIELD_VALUE_EPSILON) {
+            v4 g = gradient_at_node(T, isOp2, id2, p, fp2, NORMAL_DELTA);
+            v3 grad = {g.x, g.y, g.z};
+            v3 pp = {p.x, p.y, p.z};
+            v3 p0 = march_toward_node(T, isOp2, id2, pp, grad, &fp2);
+            v4 p00 = {p0.x, p0.y, p0.z, 0.0f};
+            v4 g0 = gradient_at_node(T, isOp2, id2, p00, fp2, NORMAL_DELTA);
+            float k = sqrtf(g0.x * g0.x + g0.y * g0.y + g0.z * g0.z);
+            float a0 = O->params[2] * C->curL;
+            v3 d3 = {p0.x - pp.x, p0.y - pp.y, p0.z - pp.z};
+            float d = sqrtf(d3.x * d3.x + d3.y * d3.y + d3.z * d3.z);
+            return fp1 + propagation_deformation(d, k, a0, O->params[0]);
+        } else if (fp2 >= ISO_VALUE && fp1 > FIELD_VALUE_EPSILON) {
+            v4 g = gradient_at_node(T, isOp1, id1, p, fp1, NORMAL_DELTA);
+            v3 grad = {g.x, g.y, g.z};
+            v3 pp = {p.x, p.y, p.z};
+            v3 p0 = march_toward_node(T, isOp1, id1, pp, grad, &fp1);
+            v4 p00 = {p0.x, p0.y, p0.z, 0.0f};
+            v4 g0 = gradient_at_node(T, isOp1, id1, p00, fp1, NORMAL_DELTA);
+            float k = sqrtf(g0.x * g0.x + g0.y * g0.y + g0.z * g0.z);
+            float a0 = O->params[3] * C->curR;
+            v3 d3 = {p0.x - pp.x, p0.y - pp.y, p0.z - pp.z};
+            float d = sqrtf(d3.x * d3.x + d3.y * d3.y + d3.z * d3.z);
+            return fp2 + propagation_deformation(d, k, a0, O->params[1]);
+        }
+        return maxf(fp1, fp2);
+    }
+    return maxf(fp1, fp2);
+}
+
 /* COMPACTBLOBTREE::fieldvalueOp (CompactBlobTree.cpp:677-891) */
 static float field_op(const Tree* T, v4 p, int id, float* storeOp, float* storePrim) {
     const PsGuiOp* O = &T->O[id];
@@ -392,6 +521,15 @@ static float field_op(const Tree* T, v4 p, int id, float* storeOp, float* storeP
                             : field_prim(T, pw, (int)(k & 0xffffu), storePrim);
     }
     switch (O->type) {
+    case PSGUI_OP_PCM:
+        if (n == 2) {
+            uint32_t k1 = T->K[O->kidStart], k2 = T->K[O->kidStart + 1];
+            res = compute_pcm(T, pw, O, (int)(k1 & 0xffffu), (int)(k2 & 0xffffu), (int)(k1 >> 16), (int)(k2 >> 16),
+                              kids[0], kids[1]);
+        } else {
+            return 0.0f;  /* before storing res: the store keeps the 0 written above */
+        }
+        break;
     case PSGUI_OP_BLEND:
         for (int i = 0; i < n; ++i) res += kids[i];
         break;
@@ -434,7 +572,13 @@ static float fieldvalue(const Tree* T, v4 p, float* so, float* sp) {
 }
 
 /* baseColorOp / baseColorPrim with the stored field values (:1108-1294) */
-static v4 color_prim(const Tree* T, int id) {
+static v4 color_op(const Tree* T, int id, const float* so, const float* sp);
+static v4 color_prim(const Tree* T, int id, const float* so, const float* sp) {
+    if (T->P[id].type == PSGUI_PRIM_INSTANCE) {  /* :1110-1118 */
+        int idxOrigin = (int)T->P[id].res1[0];
+        int isOriginOp = (int)T->P[id].res1[2];
+        return isOriginOp ? color_op(T, idxOrigin, so, sp) : color_prim(T, idxOrigin, so, sp);
+    }
     v4 c = {T->P[id].color[0], T->P[id].color[1], T->P[id].color[2], T->P[id].color[3]};
     return c;
 }
@@ -452,7 +596,7 @@ static v4 color_op(const Tree* T, int id, const float* so, const float* sp) {
             cl[i] = color_op(T, kid, so, sp);
             fv[i] = so[kid];
         } else {
-            cl[i] = color_prim(T, kid);
+            cl[i] = color_prim(T, kid, so, sp);
             fv[i] = sp[kid];
         }
     }
@@ -472,6 +616,8 @@ static v4 color_op(const Tree* T, int id, const float* so, const float* sp) {
         res.x *= r; res.y *= r; res.z *= r; res.w *= r;
         return res;
     }
+    case PSGUI_OP_PCM:  /* :1191-1200 */
+        return (fv[0] > fv[1]) ? cl[0] : cl[1];
     case PSGUI_OP_UNION:
         temp = fv[0];
         for (int i = 1; i < n; ++i)
@@ -496,7 +642,10 @@ static v4 color_op(const Tree* T, int id, const float* so, const float* sp) {
 }
 static v4 base_color(const Tree* T, const float* so, const float* sp) {
     if (T->nO > 0) return color_op(T, 0, so, sp);
-    if (T->nP > 0) return color_prim(T, 0);
+    if (T->nP > 0) {  /* m_lpPrims[0].color (:1099-1100) */
+        v4 c = {T->P[0].color[0], T->P[0].color[1], T->P[0].color[2], T->P[0].color[3]};
+        return c;
+    }
     v4 z = {0, 0, 0, 0};
     return z;
 }
@@ -722,6 +871,7 @@ typedef struct {
 
 typedef struct {
     const Tree* T;
+    PcmCtx pcm;  /* this thread's copy of the contact state */
     const int32_t* tri;
     const float* lo;
     float cs, iso, side;
@@ -732,6 +882,8 @@ typedef struct {
 
 static void* run_job(void* arg) {
     Job* J = (Job*)arg;
+    Tree TT = *J->T;
+    TT.pcm = &J->pcm;
     EdgeTable* E = malloc(sizeof(EdgeTable));
     float* cache = malloc(sizeof(float) * MAX_GRID * MAX_GRID * MAX_GRID);
     float* so = calloc(J->T->nO + 1, sizeof(float));
@@ -739,7 +891,7 @@ static void* run_job(void* arg) {
     for (uint32_t m = J->begin; m < J->end; ++m) {
         uint32_t k = m % J->dims[2], j = (m / J->dims[2]) % J->dims[1], i = m / (J->dims[2] * J->dims[1]);
         v3 o = {J->lo[0] + (float)i * J->side, J->lo[1] + (float)j * J->side, J->lo[2] + (float)k * J->side};
-        do_marching_cubes(J->T, J->tri, o, J->cs, J->iso, &J->R->mpus[m], E, cache, so, sp);
+        do_marching_cubes(&TT, J->tri, o, J->cs, J->iso, &J->R->mpus[m], E, cache, so, sp);
     }
     free(so);
     free(sp);
@@ -748,11 +900,14 @@ static void* run_job(void* arg) {
     return NULL;
 }
 
-/* CParsipOptimized::setup + run (:330-410).  *out: a Result for psgui_result_*. */
+/* CParsipOptimized::setup + run (:330-410).  *out: a Result for psgui_result_*.  pcmState
+ * (may be NULL: ISO_VALUE, not returned): the contact state the run reads, replaced by the
+ * state it leaves. */
 int psgui_polygonize(const PsGuiPrim* prims, uint32_t nP, const PsGuiOp* ops, uint32_t nO, const uint32_t* kids,
                      const PsGuiMatrix* mtx, const float lo[3], const float hi[3], float cs, float iso,
-                     const int32_t* tri, int threads, void** out) {
-    Tree T = {prims, nP, ops, nO, kids, mtx};
+                     const int32_t* tri, int threads, void** out, float* pcmState) {
+    Tree T = {prims, nP, ops, nO, kids, mtx, 0};
+    const float curL = pcmState ? pcmState[0] : ISO_VALUE, curR = pcmState ? pcmState[1] : ISO_VALUE;
     Result* R = calloc(1, sizeof(Result));
     int cells[3];
     for (int a = 0; a < 3; ++a) {
@@ -768,12 +923,22 @@ int psgui_polygonize(const PsGuiPrim* prims, uint32_t nP, const PsGuiOp* ops, ui
     Job jobs[64];
     if (threads > 64) threads = 64;
     for (int t = 0; t < threads; ++t) {
-        Job J = {&T, tri, lo, cs, iso, (float)CELLS * cs, {R->info.dims[0], R->info.dims[1], R->info.dims[2]}, R,
+        Job J = {&T, {curL, curR, curL, curR, 1}, tri, lo, cs, iso, (float)CELLS * cs,
+                 {R->info.dims[0], R->info.dims[1], R->info.dims[2]}, R,
                  (uint32_t)((uint64_t)N * t / threads), (uint32_t)((uint64_t)N * (t + 1) / threads)};
         jobs[t] = J;
         pthread_create(&th[t], NULL, run_job, &jobs[t]);
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    if (pcmState) {  /* maxima: the thread split does not matter */
+        float mL = curL, mR = curR;
+        for (int t = 0; t < threads; ++t) {
+            if (jobs[t].pcm.maxL > mL) mL = jobs[t].pcm.maxL;
+            if (jobs[t].pcm.maxR > mR) mR = jobs[t].pcm.maxR;
+        }
+        pcmState[0] = mL;
+        pcmState[1] = mR;
+    }
     for (uint32_t m = 0; m < N; ++m) {
         MpuMesh* M = &R->mpus[m];
         R->info.ctFieldEvals += M->st.fieldEvals;
@@ -826,8 +991,10 @@ void psgui_result_free(void* r) {
 
 /* fieldvalue + baseColor at n points (baseColor over the values stored by that walk) */
 void psgui_field_values(const PsGuiPrim* prims, uint32_t nP, const PsGuiOp* ops, uint32_t nO, const uint32_t* kids,
-                        const PsGuiMatrix* mtx, const float* xyz3, uint32_t n, float* out, float* col4) {
-    Tree T = {prims, nP, ops, nO, kids, mtx};
+                        const PsGuiMatrix* mtx, const float* xyz3, uint32_t n, float* out, float* col4,
+                        const float* pcmState) {
+    PcmCtx C = {pcmState ? pcmState[0] : ISO_VALUE, pcmState ? pcmState[1] : ISO_VALUE, 0.0f, 0.0f, 0};
+    Tree T = {prims, nP, ops, nO, kids, mtx, &C};
     float* so = calloc(nO + 1, sizeof(float));
     float* sp = calloc(nP + 1, sizeof(float));
     for (uint32_t i = 0; i < n; ++i) {

@@ -28,12 +28,12 @@ def lib():
         L = ctypes.CDLL(path)
         vp, u32, f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float
         L.psgui_polygonize.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp, f32, f32, vp, ctypes.c_int,
-                                       ctypes.POINTER(vp)]
+                                       ctypes.POINTER(vp), vp]
         L.psgui_polygonize.restype = ctypes.c_int
         L.psgui_result_info.argtypes = [vp, ctypes.POINTER(PsGuiInfo)]
         L.psgui_result_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.psgui_result_free.argtypes = [vp]
-        L.psgui_field_values.argtypes = [vp, u32, vp, u32, vp, vp, vp, u32, vp, vp]
+        L.psgui_field_values.argtypes = [vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
         L.psgui_set_grid_dim.argtypes = [ctypes.c_int]
         L.psgui_set_grid_dim.restype = ctypes.c_int
         L.psgui_libm_agreement.argtypes = [vp, vp, u32, vp, vp]
@@ -58,6 +58,7 @@ class GuiOracleResult:
     mpu_v: np.ndarray
     mpu_t: np.ndarray
     stats: np.ndarray
+    pcm_state: np.ndarray  # the PCM contact state the run left (left, right)
 
 
 def _tree_args(tree):
@@ -67,17 +68,20 @@ def _tree_args(tree):
 
 
 def polygonize(tree, lo, hi, cellsize: float, isovalue: float = 0.5, threads: int = 4,
-               grid_dim: int = 8) -> GuiOracleResult:
+               grid_dim: int = 8, pcm_state=None) -> GuiOracleResult:
     """CParsipOptimized::setup + run on the CPU (lattice over [lo, hi]); grid_dim is the
-    header's GRID_DIM (8 in this snapshot; 16 / 32 its other settings)."""
+    header's GRID_DIM (8 in this snapshot; 16 / 32 its other settings).  pcm_state: the PCM
+    contact state the run reads (default ISO_VALUE, as after convert); the result carries
+    the state it leaves."""
     L = lib()
     assert L.psgui_set_grid_dim(grid_dim) == 1
     lo = np.ascontiguousarray(lo, np.float32)[:3].copy()
     hi = np.ascontiguousarray(hi, np.float32)[:3].copy()
     tri = _tri_table()
     h = ctypes.c_void_p()
+    pcm = np.array([0.5, 0.5] if pcm_state is None else pcm_state, np.float32)
     L.psgui_polygonize(*_tree_args(tree), lo.ctypes.data, hi.ctypes.data, cellsize, isovalue, tri.ctypes.data,
-                       threads, ctypes.byref(h))
+                       threads, ctypes.byref(h), pcm.ctypes.data)
     info = PsGuiInfo()
     L.psgui_result_info(h, ctypes.byref(info))
     V, T, N = info.ctVertices, info.ctTriangles, info.ctLatticeMPUs
@@ -91,15 +95,17 @@ def polygonize(tree, lo, hi, cellsize: float, isovalue: float = 0.5, threads: in
                         st.ctypes.data)
     L.psgui_result_free(h)
     return GuiOracleResult(info, pos, nrm, col, tris, (off & 0xFFFFFFFF).astype(np.int64),
-                           (off >> 32).astype(np.int64), st[:N])
+                           (off >> 32).astype(np.int64), st[:N], pcm)
 
 
-def field_values(tree, xyz):
+def field_values(tree, xyz, pcm_state=None):
     L = lib()
     xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
     out = np.zeros(len(xyz), np.float32)
     col = np.zeros((len(xyz), 4), np.float32)
-    L.psgui_field_values(*_tree_args(tree), xyz.ctypes.data, len(xyz), out.ctypes.data, col.ctypes.data)
+    pcm = np.array([0.5, 0.5] if pcm_state is None else pcm_state, np.float32)
+    L.psgui_field_values(*_tree_args(tree), xyz.ctypes.data, len(xyz), out.ctypes.data, col.ctypes.data,
+                         pcm.ctypes.data)
     return out, col
 
 

@@ -267,6 +267,10 @@ def Null(**kw):  # CNullPrimitive
     return BlobNode(BlobNodeType.PRIM_NULL, **kw)
 
 
+def Instance(origin: "BlobNode", **kw):  # CInstance (PS_BlobTree/include/CInstance.h): origin's field
+    return BlobNode(BlobNodeType.PRIM_INSTANCE, params={"origin": origin}, **kw)
+
+
 def Op(kind: BlobNodeType, *children, **params) -> BlobNode:
     """An operator node; RicciBlend takes n=..., warps their factors (resX..resW)."""
     return BlobNode(BlobNodeType(kind), children=list(children), params=params)
@@ -312,10 +316,28 @@ def compute_octrees(n: BlobNode, method: str = "reference"):
     for SimdPoly (compute_octrees_reference), or "aabb", conservative world AABBs of each
     skeleton's support (8 transformed corners; an operator's box is the union)."""
     if method == "reference":
-        return compute_octrees_reference(n)
-    if method != "aabb":
+        fn = compute_octrees_reference
+    elif method == "aabb":
+        fn = compute_octrees_aabb
+    else:
         raise ValueError(f"unknown octree method {method!r}")
-    return compute_octrees_aabb(n)
+    box = fn(n)
+    if _has_instance(n):  # an Instance takes its origin's box: a second pass once every origin has one
+        box = fn(n)
+    return box
+
+
+def _has_instance(n: BlobNode) -> bool:
+    return n.node_type == BlobNodeType.PRIM_INSTANCE or any(_has_instance(c) for c in n.children)
+
+
+def _instance_box(n: BlobNode, fwd: "Matrix"):
+    """CInstance::computeOctree (CInstance.h:43-53): the origin's box (zero before the origin
+    has one), mapped like a primitive's by the accumulated forward matrix."""
+    o = n.params["origin"].octree
+    blo, bhi = (np.zeros(3, np.float32), np.zeros(3, np.float32)) if o is None else o
+    lt, ht = fwd.transform(blo), fwd.transform(bhi)
+    return np.minimum(lt, ht), np.maximum(lt, ht)
 
 
 def compute_octrees_aabb(n: BlobNode):
@@ -323,6 +345,8 @@ def compute_octrees_aabb(n: BlobNode):
         boxes = [compute_octrees_aabb(c) for c in n.children]
         lo = np.min([b[0] for b in boxes], axis=0)
         hi = np.max([b[1] for b in boxes], axis=0)
+    elif n.node_type == BlobNodeType.PRIM_INSTANCE:
+        lo, hi = _instance_box(n, n.transform.forward())
     else:
         llo, lhi = _local_support_box(n)
         fwd = n.transform.forward()
@@ -403,6 +427,8 @@ def compute_octrees_reference(n: BlobNode, branch: "Matrix | None" = None):
         else:
             for blo, bhi in boxes[1:]:
                 lo, hi = np.minimum(lo, blo), np.maximum(hi, bhi)
+    elif n.node_type == BlobNodeType.PRIM_INSTANCE:
+        lo, hi = _instance_box(n, cur)
     else:
         blo, bhi = _skeleton_bound(n)
         lt, ht = cur.transform(blo), cur.transform(bhi)

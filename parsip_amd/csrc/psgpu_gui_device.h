@@ -47,6 +47,10 @@ struct Tree {
     // box tests -- set by a kernel whose wave's points all lie in a known box
     uint64_t pm0, pm1, om0, om1;
     uint32_t masked;
+    // trees with PCM / Instance nodes (the extended walk): per operator its parent operator
+    // (0xffff: the root), and the PCM contact state the run reads (left, right)
+    const uint16_t* __restrict__ parent;
+    const float* __restrict__ pcm;
 };
 
 // Does any active lane's point lie in box b?  (A NaN coordinate counts as inside.)
@@ -104,6 +108,8 @@ struct Params {
     uint64_t* vtask;     // per mesh vertex: MPU | edge index << 32 (k_gui_edges -> k_gui_vertices)
     uint32_t nV;         // mesh vertices of the run
     PsGuiInfo* totals;
+    float* pcmState;     // extended walk: [0..1] the state the run reads (T.pcm), [2..3] the
+                         // run's maxima (atomic max), copied to [0..1] when the run ends
 };
 
 // Ricci's powf, correctly rounded through f64 (one out-of-line copy: it is large).  A far
@@ -628,9 +634,279 @@ __device__ __forceinline__ void edge_corners(int idx, int c[2][3]) {
 }
 
 // ---------------------------------------------------------------------------
+// The extended walk: trees with PCM (precise contact modelling) or Instance nodes.  The
+// interpreter's frame walk plus
+//   - Instance (fieldvaluePrim :1069-1078): the instance's backward matrix, then its origin
+//     node evaluated at that point with w = 1 (an origin operator is pushed as a frame of
+//     the same stack); its colour is the origin's colour from the main walk's stored values
+//     (baseColorPrim :1108-1122), i.e. the origin subtree walked again at the point the
+//     main walk hands the origin (the ancestor chain's op_point from the root);
+//   - PCM (fieldvalueOp :763-806, computePCM :490-570): the two kids' values, then
+//     interpenetration (both >= iso: the larger plus iso minus the smaller, the smaller
+//     raising the run's compression maximum), propagation (one >= iso, the other > 1e-3:
+//     gradientAtNode :617-643 at the point, marchTowardNode :572-592 to the other kid's
+//     iso surface, the gradient there, computePropagationDeformation :594-614 with the
+//     contact state the run started with) or the maximum; colour baseColorOp :1191-1200.
+// No culling: the sub-walks leave the wave's points.  set_tree guarantees PCM has 2 kids,
+// no PCM sits inside a PCM's kid subtree and no Instance inside an Instance's origin
+// subtree, so every sub-walk below is one level deep (LEVEL 0 the walk itself, 1 the
+// colour walk of an Instance's origin, 2 the value walk of a PCM kid).
+constexpr float kIsoValue = 0.5f;          // ISO_VALUE (_constSettings.h:10)
+constexpr float kIsoDistance = 0.454202f;  // ISO_DISTANCE (:11), marchTowardNode's first step
+
+struct PcmAcc {
+    float l, r;  // the largest compression met left / right (0: none)
+};
+
+struct XFrame {
+    Frame f;
+    int32_t inst;  // >= 0: the frame evaluates instance primitive `inst`'s origin operator
+};
+
+__device__ __forceinline__ void xinit(const Tree& T, XFrame& F, uint32_t op, V4 parentPoint, int32_t inst) {
+    init_frame(T, F.f, op, parentPoint);
+    F.inst = inst;
+}
+
+// the point an Instance hands its origin: its backward matrix applied to (p, 1), w = 1
+__device__ __forceinline__ V4 instance_point(const Tree& T, const PsGuiPrim& P, V4 p) {
+    V4 q = {p.x, p.y, p.z, 1.0f};
+    if (P.idxMtx != 0) {
+        const PsGuiMatrix& m = T.M[P.idxMtx];
+        const V4 pp = {p.x, p.y, p.z, 1.0f};
+        q.x = dot4(m.r[0], pp);
+        q.y = dot4(m.r[1], pp);
+        q.z = dot4(m.r[2], pp);
+    }
+    return q;
+}
+__device__ __forceinline__ uint32_t inst_origin(const PsGuiPrim& P) { return (uint32_t)(int)P.res1[0]; }
+__device__ __forceinline__ bool inst_origin_is_op(const PsGuiPrim& P) { return P.res1[2] != 0.0f; }
+
+template <bool COLOR>
+__device__ __forceinline__ void xfold(const PsGuiOp& O, XFrame& F, uint32_t i, float v, const float* c) {
+    if (O.type == PSGUI_OP_PCM) {  // kid 0 -> res / c, kid 1 -> aux / c0
+        if (i == 0) {
+            F.f.res = v;
+            if (COLOR) { F.f.c[0] = c[0]; F.f.c[1] = c[1]; F.f.c[2] = c[2]; F.f.c[3] = c[3]; }
+        } else {
+            F.f.aux = v;
+            if (COLOR) { F.f.c0[0] = c[0]; F.f.c0[1] = c[1]; F.f.c0[2] = c[2]; F.f.c0[3] = c[3]; }
+        }
+        return;
+    }
+    fold_k<COLOR>(O, O.type, F.f, i, v, c);
+}
+
+template <int LEVEL>
+__device__ float xwalk_value(const Tree& T, uint32_t op0, V4 parentPoint);
+
+// fieldAtNode (:646-652): a kid's value at p (a primitive kid may be an Instance)
+template <int LEVEL>
+__device__ float node_value(const Tree& T, uint32_t kid, V4 p) {
+    const uint32_t id = kid & 0xffffu;
+    if (kid >> 16) return xwalk_value<LEVEL>(T, id, p);
+    const PsGuiPrim& P = T.P[id];
+    if (P.type != PSGUI_PRIM_INSTANCE) return prim_field(T, id, p);
+    const V4 q = instance_point(T, P, p);
+    return inst_origin_is_op(P) ? xwalk_value<LEVEL>(T, inst_origin(P), q) : prim_field(T, inst_origin(P), q);
+}
+
+// gradientAtNode (:617-643): forward differences of a kid at p, (f(p + d e) - fp) * (1 / d)
+template <int LEVEL>
+__device__ V3 node_gradient(const Tree& T, uint32_t kid, V4 p, float fp) {
+    const float inv = 1.0f / kNormalDelta;
+    const float a0 = node_value<LEVEL>(T, kid, V4{p.x + kNormalDelta, p.y + 0.0f, p.z + 0.0f, p.w + 0.0f});
+    const float a1 = node_value<LEVEL>(T, kid, V4{p.x + 0.0f, p.y + kNormalDelta, p.z + 0.0f, p.w + 0.0f});
+    const float a2 = node_value<LEVEL>(T, kid, V4{p.x + 0.0f, p.y + 0.0f, p.z + kNormalDelta, p.w + 0.0f});
+    return V3{(a0 - fp) * inv, (a1 - fp) * inv, (a2 - fp) * inv};
+}
+
+// computePropagationDeformation (:594-614)
+__device__ __forceinline__ float pcm_deformation(float dist, float k, float a0, float w) {
+    const float wh = 0.5f * w, w2 = w * w, w3 = w2 * w;
+    if (dist >= 0.0f && dist < wh) {
+        const float p1 = (4.0f * (w * k - 4.0f * a0)) / w3;
+        const float p2 = (4.0f * (3.0f * a0 - w * k)) / w2;
+        const float d2 = dist * dist, d3 = dist * d2;
+        return p1 * d3 + p2 * d2 + k * dist;
+    }
+    if (dist >= wh && dist < w) return (4.0f * a0 + (dist - w) * (dist - w) * (4.0f * dist - w)) / w3;
+    return 0.0f;
+}
+
+// The propagation term of computePCM (:524-564) for the kid `kid` with value fp at p.
+template <int LEVEL>
+__device__ float pcm_propagation(const Tree& T, uint32_t kid, V4 p, float fp, float a0, float w) {
+    const V3 grad = node_gradient<LEVEL>(T, kid, p, fp);
+    const V3 pp = {p.x, p.y, p.z};
+    // marchTowardNode (:572-592): shrink-wrap steps along the gradient toward f = iso
+    int dir = (fp < kIsoValue) ? 1 : -1;
+    float step = kIsoDistance;
+    V3 q = pp;
+    for (int it = 0; it < PSGUI_PCM_MARCH_MAX && !(((kIsoValue - kFieldEps) < fp) && (fp < (kIsoValue + kFieldEps)));
+         ++it) {
+        const float s = step * (float)dir;
+        q.x += grad.x * s;
+        q.y += grad.y * s;
+        q.z += grad.z * s;
+        fp = node_value<LEVEL>(T, kid, V4{q.x, q.y, q.z, 0.0f});
+        const int dir2 = (fp < kIsoValue) ? 1 : -1;
+        if (dir != dir2) step *= 0.5f;
+        dir = dir2;
+    }
+    const V3 g0 = node_gradient<LEVEL>(T, kid, V4{q.x, q.y, q.z, 0.0f}, fp);
+    const float k = sqrtf(g0.x * g0.x + g0.y * g0.y + g0.z * g0.z);
+    const float dx = q.x - pp.x, dy = q.y - pp.y, dz = q.z - pp.z;  // pp.distance(p0)
+    const float d = sqrtf(dx * dx + dy * dy + dz * dz);
+    return pcm_deformation(d, k, a0, w);
+}
+
+__device__ __forceinline__ const float* node_oct(const Tree& T, uint32_t kid, bool hi) {
+    const uint32_t id = kid & 0xffffu;
+    return (kid >> 16) ? (hi ? T.O[id].octHi : T.O[id].octLo) : (hi ? T.P[id].octHi : T.P[id].octLo);
+}
+
+// computePCM (:490-570) over the kids' values fp1, fp2 at p (the PCM's own point)
+template <int LEVEL>
+__device__ float pcm_field(const Tree& T, const PsGuiOp& O, V4 p, float fp1, float fp2, PcmAcc* acc) {
+    const uint32_t k1 = T.K[O.kidStart], k2 = T.K[O.kidStart + 1];
+    const float *lo1 = node_oct(T, k1, false), *hi1 = node_oct(T, k1, true);
+    const float *lo2 = node_oct(T, k2, false), *hi2 = node_oct(T, k2, true);
+    const bool crossed = !((lo1[0] >= hi2[0]) || (hi1[0] <= lo2[0]) || (lo1[1] >= hi2[1]) || (hi1[1] <= lo2[1]) ||
+                           (lo1[2] >= hi2[2]) || (hi1[2] <= lo2[2]));  // intersects (_GlobalFunctions.h:34-44)
+    if (!crossed) return maxf(fp1, fp2);
+    if (fp1 >= kIsoValue && fp2 >= kIsoValue) {  // interpenetration
+        if (fp1 > fp2) {
+            if (acc && fp2 > acc->l) acc->l = fp2;
+            return fp1 + (kIsoValue - fp2);
+        }
+        if (acc && fp1 > acc->r) acc->r = fp1;
+        return fp2 + (kIsoValue - fp1);
+    }
+    if constexpr (LEVEL >= 2) {
+        return maxf(fp1, fp2);  // not reached: set_tree rejects a PCM inside a PCM's kids
+    } else {
+        if (fp1 >= kIsoValue && fp2 > kFieldEps) return fp1 + pcm_propagation<2>(T, k2, p, fp2, O.params[2] * T.pcm[0], O.params[0]);
+        if (fp2 >= kIsoValue && fp1 > kFieldEps) return fp2 + pcm_propagation<2>(T, k1, p, fp1, O.params[3] * T.pcm[1], O.params[1]);
+        return maxf(fp1, fp2);
+    }
+}
+
+template <bool COLOR, int LEVEL>
+__device__ float xwalk(const Tree& T, uint32_t op0, V4 parentPoint, V4 rootPoint, float* colOut, PcmAcc* acc);
+
+// An Instance's colour: its origin operator's colour in the main walk (LEVEL 0 only: no
+// Instance sits inside an origin subtree).
+__device__ void origin_colour(const Tree& T, uint32_t X, V4 rootPoint, float* c) {
+    uint32_t path[PSGUI_MAX_DEPTH];
+    int n = 0;
+    for (uint32_t a = T.parent[X]; a != 0xffffu && n < PSGUI_MAX_DEPTH; a = T.parent[a]) path[n++] = a;
+    V4 q = rootPoint;
+    for (int j = n - 1; j >= 0; --j) q = op_point(T, T.O[path[j]], q);
+    (void)xwalk<true, 1>(T, X, q, q, c, nullptr);
+}
+
+// fieldvalueOp from operator op0 (its parent's point `parentPoint`) and, with COLOR, its
+// baseColorOp over the same walk's values.
+template <bool COLOR, int LEVEL>
+__device__ float xwalk(const Tree& T, uint32_t op0, V4 parentPoint, V4 rootPoint, float* colOut, PcmAcc* acc) {
+    XFrame st[PSGUI_MAX_DEPTH];
+    int sp = 0;
+    xinit(T, st[0], op0, parentPoint, -1);
+    for (;;) {
+        XFrame& F = st[sp];
+        const PsGuiOp& O = T.O[F.f.op];
+        if (F.f.next < (uint32_t)O.ctKids) {
+            const uint32_t k = T.K[O.kidStart + F.f.next];
+            const uint32_t i = F.f.next++;
+            const uint32_t id = k & 0xffffu;
+            if (k >> 16) {
+                xinit(T, st[++sp], id, F.f.p, -1);
+                continue;
+            }
+            const PsGuiPrim& P = T.P[id];
+            if (P.type != PSGUI_PRIM_INSTANCE) {
+                xfold<COLOR>(O, F, i, prim_field(T, id, F.f.p), P.color);
+                continue;
+            }
+            const V4 q = instance_point(T, P, F.f.p);
+            const uint32_t o = inst_origin(P);
+            if (inst_origin_is_op(P)) {
+                xinit(T, st[++sp], o, q, (int32_t)id);
+                continue;
+            }
+            xfold<COLOR>(O, F, i, prim_field(T, o, q), T.P[o].color);  // a primitive origin's colour
+            continue;
+        }
+        float v;
+        if (O.type == PSGUI_OP_PCM) {
+            v = pcm_field<LEVEL>(T, O, F.f.p, F.f.res, F.f.aux, acc);
+            if (COLOR && !(F.f.res > F.f.aux)) {
+                F.f.c[0] = F.f.c0[0]; F.f.c[1] = F.f.c0[1]; F.f.c[2] = F.f.c0[2]; F.f.c[3] = F.f.c0[3];
+            }
+        } else {
+            v = finalize_k<COLOR>(O, O.type, F.f);
+        }
+        if (sp == 0) {
+            if (COLOR) { colOut[0] = F.f.c[0]; colOut[1] = F.f.c[1]; colOut[2] = F.f.c[2]; colOut[3] = F.f.c[3]; }
+            return v;
+        }
+        const float* c = F.f.c;
+        float ic[4];
+        if constexpr (COLOR && LEVEL == 0) {
+            if (F.inst >= 0) {
+                origin_colour(T, F.f.op, rootPoint, ic);
+                c = ic;
+            }
+        }
+        XFrame& Pf = st[--sp];
+        xfold<COLOR>(T.O[Pf.f.op], Pf, Pf.f.next - 1, v, c);
+    }
+}
+
+template <int LEVEL>
+__device__ float xwalk_value(const Tree& T, uint32_t op0, V4 parentPoint) {
+    return xwalk<false, LEVEL>(T, op0, parentPoint, parentPoint, nullptr, nullptr);
+}
+
+// COMPACTBLOBTREE::fieldvalue / baseColor (:476-487, :1095-1106) over the extended walk;
+// acc (may be null) collects the interpenetration maxima of this evaluation.
+struct ExtField {
+    template <bool COLOR>
+    __device__ static float eval(const Tree& T, float x, float y, float z, float* colOut, PcmAcc* acc = nullptr) {
+        const V4 p = {x, y, z, 0.0f};
+        if (T.nO == 0) {
+            if (COLOR && T.nP) { colOut[0] = T.P[0].color[0]; colOut[1] = T.P[0].color[1]; colOut[2] = T.P[0].color[2]; colOut[3] = T.P[0].color[3]; }
+            return T.nP ? node_value<2>(T, 0u, p) : 0.0f;
+        }
+        return xwalk<COLOR, 0>(T, 0, p, p, colOut, acc);
+    }
+    template <bool COLOR>
+    __device__ static float eval_call(const Tree& T, float x, float y, float z, float* colOut, PcmAcc* acc = nullptr) {
+        return eval<COLOR>(T, x, y, z, colOut, acc);
+    }
+};
+template <class EV>
+struct IsExt {
+    static constexpr bool value = false;
+};
+template <>
+struct IsExt<ExtField> {
+    static constexpr bool value = true;
+};
+
+// One wave's compression maxima into the run's (all 64 lanes active).
+__device__ __forceinline__ void pcm_publish(const Params& p, const PcmAcc& a) {
+    const float l = wave_max_f(a.l), r = wave_max_f(a.r);
+    if ((threadIdx.x & 63u) == 0u) {
+        if (l > 0.0f) atomicMax(reinterpret_cast<int*>(p.pcmState + 2), __float_as_int(l));
+        if (r > 0.0f) atomicMax(reinterpret_cast<int*>(p.pcmState + 3), __float_as_int(r));
+    }
+}
 
 // ---------------------------------------------------------------------------
-// Kernel bodies over an evaluator EV (InterpField or a generated JitField).
+// Kernel bodies over an evaluator EV (InterpField, ExtField or a generated JitField).
 //
 // One wavefront per MPU: the octree test against every primitive (:164-183), the 8^3
 // field cache (lane = (y, z), one walk per x), configs with `f > iso`, per-MPU counts.
@@ -663,15 +939,19 @@ __device__ __forceinline__ void classify_body(const Params& p, float* fv) {
     const float yHi = o[1] + p.cs * 7.0f, zHi = o[2] + p.cs * 7.0f;
     const int j = lane >> 3, k = lane & 7;
     const float y = o[1] + p.cs * (float)j, z = o[2] + p.cs * (float)k;
+    PcmAcc acc{0.0f, 0.0f};
 #pragma unroll 1
     for (int i = 0; i < kG; ++i) {
         const float x = o[0] + p.cs * (float)i;
         Tree T = p.T;
         mask_for_box(T, x, o[1], o[2], x, yHi, zHi);
-        const float f = EV::template eval<false>(T, x, y, z, nullptr);
+        float f;
+        if constexpr (IsExt<EV>::value) f = EV::template eval<false>(T, x, y, z, nullptr, &acc);
+        else f = EV::template eval<false>(T, x, y, z, nullptr);
         fv[corner_of(i, j, k)] = f;
         p.fvc[(size_t)m * kCorners + corner_of(i, j, k)] = f;
     }
+    if constexpr (IsExt<EV>::value) pcm_publish(p, acc);  // every corner is a reference evaluation
     __syncthreads();
     uint32_t nv = 0, nt = 0, nc = 0;
     for (int cell = lane; cell < kCells; cell += 64) {
@@ -733,6 +1013,13 @@ __device__ __forceinline__ void vertices_body(const Params& p) {
     float outF = 0.0f;
     int itFinal = PSGUI_ITERATIONS;
     bool done = !valid;
+    // extended walk: the compression maxima of the evaluations the reference makes (lane 3's
+    // x of every round; lanes 0-2's gradient samples only when the iteration goes on)
+    PcmAcc run{0.0f, 0.0f};
+    auto commit = [&](const PcmAcc& e) {
+        run.l = e.l > run.l ? e.l : run.l;
+        run.r = e.r > run.r ? e.r : run.r;
+    };
     // every lane stays in the loop until the whole wave is done (finished quads walk their
     // last point again and ignore it), so each round's culling masks come from all 64 lanes
     for (int r = 0;; ++r) {
@@ -745,10 +1032,14 @@ __device__ __forceinline__ void vertices_body(const Params& p) {
         }
         Tree T = p.T;
         wave_mask(T, px, py, pz);
-        const float f = EV::template eval_call<false>(T, px, py, pz, nullptr);
+        PcmAcc e{0.0f, 0.0f};
+        float f;
+        if constexpr (IsExt<EV>::value) f = EV::template eval_call<false>(T, px, py, pz, nullptr, &e);
+        else f = EV::template eval_call<false>(T, px, py, pz, nullptr);
         const float fx = __shfl(f, base + 0), fy = __shfl(f, base + 1), fz = __shfl(f, base + 2);
         const float fc = __shfl(f, base + 3);
         if (done) continue;
+        if (IsExt<EV>::value && q == 3) commit(e);
         if (r >= 1) {  // fc = f(x) = the step of iteration r - 1's outF
             outF = fc;
             if (fabsf(outF - iso) < kFieldEps) {
@@ -761,6 +1052,7 @@ __device__ __forceinline__ void vertices_body(const Params& p) {
                 continue;
             }
         }
+        if (IsExt<EV>::value && q < 3) commit(e);
         const float fp = fc;
         float gx = fx, gy = fy, gz = fz;
         gx -= fp; gy -= fp; gz -= fp;
@@ -781,7 +1073,15 @@ __device__ __forceinline__ void vertices_body(const Params& p) {
     float c4[4];
     Tree T = p.T;
     wave_mask(T, px, py, pz);
-    const float f = EV::template eval_call<true>(T, px, py, pz, c4);
+    float f;
+    if constexpr (IsExt<EV>::value) {
+        PcmAcc e{0.0f, 0.0f};  // normal samples; lane 3 re-walks x (the same maxima)
+        f = EV::template eval_call<true>(T, px, py, pz, c4, &e);
+        if (valid) commit(e);
+        pcm_publish(p, run);
+    } else {
+        f = EV::template eval_call<true>(T, px, py, pz, c4);
+    }
     float nx = __shfl(f, base + 0), ny = __shfl(f, base + 1), nz = __shfl(f, base + 2);
     const float col0 = __shfl(c4[0], base + 3), col1 = __shfl(c4[1], base + 3);
     const float col2 = __shfl(c4[2], base + 3), col3 = __shfl(c4[3], base + 3);

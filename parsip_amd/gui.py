@@ -35,7 +35,7 @@ ERR_PRIMS_OVERFLOW = -2
 ERR_KIDS_OVERFLOW = -3
 ERR_PARAM_ERROR = -4
 ERR_NODE_NOT_RECOGNIZED = -5
-RET_UNSUPPORTED = -7  # PSGUI_RET_UNSUPPORTED (the device walk: Instance, PCM, empty operators)
+RET_UNSUPPORTED = -7  # PSGUI_RET_UNSUPPORTED (parsip_gpu_gui.h: empty operators, depth, PCM / Instance limits)
 MAX_COMPACT_KIDS_COUNT = 1024
 MIN_BLOB_NODES = 32
 ISO_VALUE = 0.5
@@ -55,7 +55,7 @@ assert PRIM_DTYPE.itemsize == 128 and OP_DTYPE.itemsize == 80 and MTX_DTYPE.item
 _OPS = {B.OP_UNION, B.OP_BLEND, B.OP_DIF, B.OP_SMOOTHDIF, B.OP_INTERSECT, B.OP_PCM, B.OP_RICCIBLEND,
         B.OP_WARPTWIST, B.OP_WARPTAPER, B.OP_WARPBEND, B.OP_WARPSHEAR}
 _PRIMS = {B.PRIM_POINT, B.PRIM_LINE, B.PRIM_RING, B.PRIM_DISC, B.PRIM_CYLINDER, B.PRIM_CUBE, B.PRIM_TRIANGLE,
-          B.PRIM_QUADRICPOINT, B.PRIM_NULL}
+          B.PRIM_QUADRICPOINT, B.PRIM_NULL, B.PRIM_INSTANCE}
 
 
 class PsGuiInfo(ctypes.Structure):
@@ -72,6 +72,16 @@ assert ctypes.sizeof(PsGuiInfo) == 56
 def QuadricPoint(position, radius, scale, **kw):  # CQuadricPoint (getFieldRadius, getFieldScale)
     return bt.BlobNode(B.PRIM_QUADRICPOINT, params={"position": position, "radius": radius, "scale": scale},
                        **kw)
+
+
+def Pcm(left, right, propagate_left=None, propagate_right=None, alpha_left=0.5, alpha_right=0.5, **kw):
+    """CPcm (PS_BlobTree/include/CPcm.h): precise contact between two kids; the defaults are
+    resetParams' PCM_PROPAGATION_WIDTH = 0.5 * ISO_DISTANCE and PCM_ATTENUATION = 0.5
+    (_constSettings.h:14-15)."""
+    w = float(np.float32(0.5) * np.float32(0.454202))
+    return bt.Op(B.OP_PCM, left, right, propagate_left=w if propagate_left is None else propagate_left,
+                 propagate_right=w if propagate_right is None else propagate_right, alpha_left=alpha_left,
+                 alpha_right=alpha_right, **kw)
 
 
 @dataclass
@@ -116,6 +126,8 @@ def compact_blobtree(root: bt.BlobNode | None, octrees: str = "reference"):
         bt.compute_octrees(root, octrees)
     prims, ops, kids = [], [], []
     mtx = [np.eye(4, dtype=np.float32)]
+    converted = []  # m_lstConvertedIds: (node, compact id) in conversion order
+    instances = []  # (prim index, origin node)
 
     def matrix_index(n) -> int:  # :118-135 / :266-283
         back = n.transform.backward()
@@ -124,7 +136,7 @@ def compact_blobtree(root: bt.BlobNode | None, octrees: str = "reference"):
         mtx.append(np.stack([back.row(r) for r in range(4)]))
         return len(mtx) - 1
 
-    def rec(n: bt.BlobNode):
+    def convert_node(n: bt.BlobNode):  # convert(CBlobNode*, parentID) (:93-408)
         lo, hi = n.octree
         if n.is_operator():
             cur = len(ops)
@@ -187,11 +199,28 @@ def compact_blobtree(root: bt.BlobNode | None, octrees: str = "reference"):
             p["res1"], p["res2"] = [_F(pr["radius"])] * 4, [_F(pr["scale"])] * 4
         elif t == B.PRIM_NULL:
             p["pos"] = _v4((0.0, 0.0, 0.0))
+        elif t == B.PRIM_INSTANCE:  # :383-391: (-1, origin id, origin isOp, origin type)
+            o = pr["origin"]
+            p["res1"] = [_F(-1.0), _F(o.node_id), _F(1.0 if o.is_operator() else 0.0), _F(int(o.node_type))]
+            instances.append((cur, o))
         else:
             return ERR_NODE_NOT_RECOGNIZED, 0
         return cur, 0
 
+    def rec(n):  # every converted node's (node, id) pair, in the reference's order (:404)
+        r = convert_node(n)
+        if r[0] >= 0:
+            converted.append((n, r[0]))
+        return r
+
     code, _ = rec(root)
+    # updateInstanceNodes (:410-431): the origin's compact id, found by its node (the
+    # reference matches the unique node id; identity is the same here, ids may be unset)
+    for idx, o in instances:
+        for n, cid in converted:
+            if n is o:
+                prims[idx]["res1"][0] = _F(cid)
+                break
     tree = CompactTree(np.array(prims, PRIM_DTYPE), np.array(ops, OP_DTYPE), np.array(kids, np.uint32),
                        np.array([(m,) for m in mtx], MTX_DTYPE), root.octree)
     return code, tree
@@ -220,6 +249,8 @@ _SIG = {
     "psgpu_gui_jit_status": (["vp", "i32"], "i32"),
     "psgpu_gui_jit_compile": (["vp", "u32", "vp", "u32", "vp", "u32", "vp", "u32", "i32", "vp", "size"], "long"),
     "psgpu_gui_cull_boxes": (["vp", "u32", "vp", "u32", "vp", "u32", "vp", "u32", "vp", "vp"], "i32"),
+    "psgpu_gui_get_pcm_state": (["vp", "vp"], "i32"),
+    "psgpu_gui_set_pcm_state": (["vp", "vp"], "i32"),
 }
 OPT_JIT = 1
 OPT_CULL = 2
@@ -369,6 +400,19 @@ class ParsipOptimized:
                    "psgpu_gui_download")
         return GuiMesh(pos, nrm, col, tris, (off & 0xFFFFFFFF).astype(np.int64), (off >> 32).astype(np.int64),
                        st[:N])
+
+    @property
+    def pcm_state(self) -> np.ndarray:
+        """The PCM contact state (maxCompressionLeft, Right) the next run reads
+        (include/parsip_gpu_gui.h: a run reads the state it started with and leaves the
+        largest compression it met)."""
+        s = np.zeros(2, np.float32)
+        gpu._check(self._L.psgpu_gui_get_pcm_state(self._g, s.ctypes.data), "psgpu_gui_get_pcm_state")
+        return s
+
+    def set_pcm_state(self, state) -> None:
+        s = np.ascontiguousarray(state, np.float32)[:2].copy()
+        gpu._check(self._L.psgpu_gui_set_pcm_state(self._g, s.ctypes.data), "psgpu_gui_set_pcm_state")
 
     def field_values(self, xyz: np.ndarray):
         """COMPACTBLOBTREE::fieldvalue + baseColor at points: (values, rgba)."""

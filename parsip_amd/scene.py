@@ -11,7 +11,10 @@ Distrib/train_corrected.scene, say SkeletonType), the affine transform AffineSca
 AffineRotate (quaternion x, y, z, w) / AffineTranslate and the material
 (CBlobNode::loadGenericInfoScript, CBlobTree.cpp:123-149), then the skeleton's own
 fields (CSkeleton*.h loadScript: position, direction, radius, height, side, start,
-end, corner0..2).  Lines end in NUL CR LF in files the reference wrote.
+end, corner0..2).  PCM reads its four widths / attenuations (CPcm.h:93-101); an
+INSTANCE primitive names its origin by OriginalNodeIndex (CInstance.h:69-75, resolved with
+findNodeByID, CLayerManager.cpp:782-793; here after the whole layer is read, so an origin
+may also come later in the file).  Lines end in NUL CR LF in files the reference wrote.
 """
 from __future__ import annotations
 
@@ -31,6 +34,7 @@ OPERATOR_NAMES = {
 PRIMITIVE_NAMES = {
     "POINT": B.PRIM_POINT, "LINE": B.PRIM_LINE, "CYLINDER": B.PRIM_CYLINDER, "DISC": B.PRIM_DISC,
     "RING": B.PRIM_RING, "CUBE": B.PRIM_CUBE, "TRIANGLE": B.PRIM_TRIANGLE, "NULL": B.PRIM_NULL,
+    "INSTANCE": B.PRIM_INSTANCE,
 }
 
 
@@ -67,6 +71,15 @@ def _ints(s: str) -> list:
 class _Reader:
     def __init__(self, sections: dict):
         self.s = sections
+        self.by_id: dict = {}
+        self.instances: list = []  # (Instance node, origin id)
+
+    def resolve_instances(self) -> None:
+        for n, oid in self.instances:
+            if oid not in self.by_id:
+                raise SceneError(f"Instance BLOBNODE {n.node_id}: unable to find origin node id {oid}")
+            n.params["origin"] = self.by_id[oid]
+        self.instances = []
 
     def sec(self, nid: int) -> dict | None:
         return self.s.get(f"BLOBNODE {nid}")
@@ -93,8 +106,13 @@ class _Reader:
             params = {}
             if OPERATOR_NAMES[name] == B.OP_RICCIBLEND:
                 params["n"] = float(sec.get("power", "2"))
+            elif OPERATOR_NAMES[name] == B.OP_PCM:  # readFloat's default is 0 (PS_AppConfig.h:60)
+                for key, k in (("Propagate Left", "propagate_left"), ("Propagate Right", "propagate_right"),
+                               ("Attenuate Left", "alpha_left"), ("Attenuate Right", "alpha_right")):
+                    params[k] = float(sec.get(key, "0"))
             n = bt.Op(OPERATOR_NAMES[name], *[self.node(i, depth + 1) for i in ids], **params)
             n.node_id = nid
+            self.by_id[nid] = n
             return n
         name = (sec.get("PrimitiveType") or sec.get("SkeletonType") or "").upper()
         if name not in PRIMITIVE_NAMES:
@@ -129,9 +147,13 @@ class _Reader:
             n = bt.Cube(v3("position"), f1("side"), **kw)
         elif t == B.PRIM_TRIANGLE:
             n = bt.Triangle(v3("corner0"), v3("corner1"), v3("corner2"), **kw)
+        elif t == B.PRIM_INSTANCE:
+            n = bt.Instance(None, **kw)
+            self.instances.append((n, int(float(sec.get("OriginalNodeIndex", "-1")))))
         else:
             n = bt.Null(**kw)
         n.node_id = nid
+        self.by_id[nid] = n
         return n
 
 
@@ -147,7 +169,12 @@ def load_scene(path_or_text: str, from_text: bool = False) -> list:
     roots = _ints(g.get("RootIDs", "()"))
     n_layers = int(float(g.get("NumLayers", len(roots))))
     rd = _Reader(sections)
-    return [rd.node(r) for r in roots[:n_layers] if r >= 0]
+    layers = []
+    for r in roots[:n_layers]:
+        if r >= 0:
+            layers.append(rd.node(r))
+            rd.resolve_instances()
+    return layers
 
 
 def count_nodes(n: bt.BlobNode) -> tuple:

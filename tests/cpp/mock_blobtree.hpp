@@ -106,6 +106,12 @@ public:
     float getFieldScale() const { return scale; }
 };
 
+class CInstance : public CBlobNode {  // CInstance.h:11-82
+public:
+    CBlobNode* origin = nullptr;
+    CBlobNode* getOriginalNode() const { return origin; }
+};
+
 class CPcm : public CBlobNode {
 public:
     float getPropagateLeft() const { return res[0]; }

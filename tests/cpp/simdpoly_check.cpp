@@ -47,6 +47,8 @@ CBlobNode* read_node(std::istream& in, std::vector<std::unique_ptr<CBlobNode>>& 
         q->radius = v[35];
         q->scale = v[36];
         n = q;
+    } else if (type == 13) {  // Instance: the origin's node id in the first skeleton slot
+        n = new CInstance();
     } else if (type >= 14) {
         switch (type) {
         case 19: n = new CRicciBlend(); break;
@@ -90,6 +92,17 @@ CBlobNode* read_node(std::istream& in, std::vector<std::unique_ptr<CBlobNode>>& 
     for (int k = 0; k < 4; ++k) n->res[k] = v[26 + k];
     for (int c = 0; c < nk; ++c) n->kids.push_back(read_node(in, own));
     return n;
+}
+
+// Instances name their origin by node id (OriginalNodeIndex, findNodeByID)
+void resolve_instances(std::vector<std::unique_ptr<CBlobNode>>& own) {
+    for (auto& n : own)
+        if (n->type == 13)
+            for (auto& m : own)
+                if (m->id == (int)n->res[0]) {
+                    static_cast<CInstance*>(n.get())->origin = m.get();
+                    break;
+                }
 }
 
 template <class T>
@@ -148,6 +161,7 @@ int main(int argc, char** argv) {
         std::vector<std::unique_ptr<CBlobNode>> own;
         CBlobNode* root = read_node(in, own);
         if (!root) return 65;
+        resolve_instances(own);
         if (mode == "gui-tree") {
             PS::COMPACTBLOBTREEGpu tree;
             const int code = tree.convert(root);

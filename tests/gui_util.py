@@ -81,6 +81,41 @@ def random_tree(seed: int, n_prims: int = 12, warps: bool = True, op_transforms:
     return root
 
 
+def _subtrees(n):
+    yield n
+    for c in n.children:
+        yield from _subtrees(c)
+
+
+def random_ext_tree(seed: int, n_prims: int = 5):
+    """A random tree with PCM and Instance nodes as the compat mode accepts them: a PCM over
+    two random subtrees (one of its kids may be an Instance), Instances of a random operator
+    and of a random primitive of those subtrees under their own transforms, and the rest
+    blended or united with them."""
+    rng = np.random.default_rng(1000 + seed)
+    a = random_tree(2 * seed + 1, n_prims=n_prims, warps=seed % 2 == 0)
+    b = random_tree(2 * seed + 2, n_prims=max(2, n_prims - 1), warps=False)
+    ops_a = [n for n in _subtrees(a) if n.is_operator()]
+    prims_b = [n for n in _subtrees(b) if not n.is_operator()]
+    x = ops_a[int(rng.integers(len(ops_a)))]
+    y = prims_b[int(rng.integers(len(prims_b)))]
+    kid2 = b if seed % 3 else bt.Instance(y, transform=_rand_affine(rng, 0.4),
+                                          material=bt.Material(diffused=(0.1, 0.9, 0.2, 1.0)))
+    pcm = gui.Pcm(a, kid2, propagate_left=float(rng.uniform(0.1, 0.6)), propagate_right=float(rng.uniform(0.1, 0.6)),
+                  alpha_left=float(rng.uniform(0.2, 1.0)), alpha_right=float(rng.uniform(0.2, 1.0)))
+    if rng.random() < 0.4:
+        pcm.transform = _rand_affine(rng, 0.5)
+    inst_x = bt.Instance(x, transform=_rand_affine(rng, 0.6))
+    inst_y = bt.Instance(y, transform=_rand_affine(rng, 0.6))
+    kind = OPS[rng.integers(len(OPS))]
+    params = {"n": 2.0} if kind == B.OP_RICCIBLEND else {}
+    rest = bt.Op(kind, inst_x, _rand_prim(rng, PRIM_KINDS[:8]), **params)
+    root = bt.Op(B.OP_UNION if seed % 2 else B.OP_BLEND, pcm, rest, inst_y)
+    if kid2 is not b:  # keep b in the tree: the Instance's origin must be converted
+        root.children.append(b)
+    return root
+
+
 def bits(a):
     """fp32 bit patterns, NaNs canonical: an invalid operation yields the negative default
     NaN on x86 SSE and the positive one on CDNA, the same result in IEEE terms."""

@@ -75,6 +75,8 @@ def write_tree(root: bt.BlobNode, path: str) -> None:
             q[0:3], q[3:6], q[6:9] = p["corners"]
         elif t == B.PRIM_QUADRICPOINT:
             q[0:3], q[9], q[10] = p["position"], p["radius"], p["scale"]
+        elif t == B.PRIM_INSTANCE:
+            q[0] = float(p["origin"].node_id)
         vals = [*_v3(lo), *_v3(hi), *_v3(n.material.diffused[:3]), 1.0 if back.is_identity() else 0.0,
                 *[float(x) for x in rows], *[float(np.float32(x)) for x in q],
                 float(np.float32(n.material.diffused[3])), float(n.node_id)]
@@ -267,14 +269,27 @@ def _walk(n):
         yield from _walk(c)
 
 
-@pytest.mark.parametrize("which", ["train", "all_types"])
+def gui_ext_tree():
+    """PCM and Instances (of an operator and of a primitive) over the all-types tree."""
+    from parsip_amd import gui
+
+    t = gui_all_types_tree()
+    x, y = t.children[-1], t.children[-1].children[0]
+    t.children.append(gui.Pcm(bt.Point((0.0, 0.0, 0.0)), bt.Instance(y), alpha_left=0.7))
+    t.children.append(bt.Instance(x, transform=bt.Affine((1, 1, 1), (0, 0, 0, 1), (0.4, 0.0, 0.0))))
+    for i, n in enumerate(_walk(t)):
+        n.node_id = 100 + i
+    return t
+
+
+@pytest.mark.parametrize("which", ["train", "all_types", "pcm_instance"])
 def test_cpp_compact_tree_matches_python(exe, tmp_path, which):
     """CompactTreeT<Api>::convert over the mock BlobTree gives the same COMPACTBLOBTREE arrays,
     byte for byte, as parsip_amd/gui.py::compact_blobtree (n-ary operators kept)."""
     from parsip_amd import gui, scene
 
     root = (scene.load_scene(os.path.join(GOLDEN, "train_corrected.scene"))[0] if which == "train"
-            else gui_all_types_tree())
+            else gui_all_types_tree() if which == "all_types" else gui_ext_tree())
     bt.compute_octrees(root)
     code, parts = cpp_compact(exe, root, tmp_path)
     pcode, tree = gui.compact_blobtree(root)

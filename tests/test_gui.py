@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import psgui
-from gui_util import assert_gui_mesh_equal, bits, random_tree
+from gui_util import assert_gui_mesh_equal, bits, random_ext_tree, random_tree
 from parsip_amd import blobtree as bt
 from parsip_amd import gui, scene
 
@@ -170,6 +170,173 @@ def test_cull_boxes_are_conservative():
     assert checked > 40, checked
 
 
+def _pcm_pair():
+    """Two blobs in contact under a PCM: an operator kid and a primitive kid."""
+    a = bt.Op(B.OP_BLEND, bt.Point((0, 0, 0)), bt.Point((0.3, 0, 0)),
+              material=bt.Material(diffused=(1.0, 0.0, 0.0, 1.0)))
+    a.children[1].material = bt.Material(diffused=(1.0, 0.5, 0.0, 1.0))
+    b = bt.Point((0.55, 0.1, 0.0), material=bt.Material(diffused=(0.0, 0.0, 1.0, 1.0)))
+    return bt.Op(B.OP_UNION, gui.Pcm(a, b, alpha_left=0.7, alpha_right=0.9))
+
+
+def test_convert_pcm_and_instance():
+    """COMPACTBLOBTREE::convert of PCM (params :168-177) and Instance (res1 :383-391, the
+    compact id resolved by updateInstanceNodes :410-431)."""
+    code, tree = gui.compact_blobtree(_pcm_pair())
+    assert code == 0 and tree.ops[1]["type"] == B.OP_PCM
+    w = np.float32(0.5) * np.float32(0.454202)  # PCM_PROPAGATION_WIDTH
+    assert np.array_equal(tree.ops[1]["params"], np.array([w, w, 0.7, 0.9], np.float32))
+    x = bt.Op(B.OP_BLEND, bt.Point((0, 0, 0)), bt.Point((0.3, 0, 0)))
+    x.node_id = 17
+    p = bt.Point((0, 0.5, 0))
+    p.node_id = 23
+    root = bt.Op(B.OP_UNION, bt.Instance(x), x, bt.Instance(p), p)
+    code, tree = gui.compact_blobtree(root)
+    assert code == 0
+    inst = tree.prims[tree.prims["type"] == B.PRIM_INSTANCE]
+    # origin x is operator 1, origin p is primitive 4 (DFS: inst, x's two points, inst, p)
+    assert inst["res1"].tolist() == [[1.0, 17.0, 1.0, float(B.OP_BLEND)], [4.0, 23.0, 0.0, float(B.PRIM_POINT)]]
+
+
+def test_oracle_pcm_contact_state_is_order_free():
+    """The defined contact-state order (include/parsip_gpu_gui.h): a run reads the state it
+    started with, so its mesh and the state it leaves do not depend on how the MPUs are
+    split over threads (the reference's running maximum per TBB body does); the
+    interpenetration raises the state above ISO_VALUE and the next run's propagation
+    (a0 = alpha x state) then differs."""
+    _, tree = gui.compact_blobtree(_pcm_pair())
+    runs = [psgui.polygonize(tree, *tree.root_octree, 0.04, 0.5, threads=t) for t in (1, 3, 8)]
+    for r in runs[1:]:
+        assert_gui_mesh_equal(r, runs[0], "thread split")
+        assert np.array_equal(r.pcm_state, runs[0].pcm_state)
+    s1 = runs[0].pcm_state
+    assert s1[0] > 0.5 and s1[1] > 0.5, s1
+    r2 = psgui.polygonize(tree, *tree.root_octree, 0.04, 0.5, threads=8, pcm_state=s1)
+    assert not (len(r2.pos) == len(runs[0].pos) and np.array_equal(bits(r2.pos), bits(runs[0].pos)))
+    assert np.all(r2.pcm_state >= s1)
+    # probes read the state and leave it alone; the propagation region sees it
+    xyz = np.random.default_rng(3).uniform(*tree.root_octree, size=(4000, 3)).astype(np.float32)
+    f1, _ = psgui.field_values(tree, xyz)
+    f2, _ = psgui.field_values(tree, xyz, pcm_state=s1)
+    assert 0 < np.count_nonzero(f1 != f2) < len(xyz)
+
+
+def test_oracle_instance_is_its_origin_moved():
+    """An Instance evaluates its origin at its backward-transformed point (:1069-1078): the
+    field of Instance(x) translated by t at p equals x's field at p - t (to rounding)."""
+    x = bt.Op(B.OP_RICCIBLEND, bt.Point((0, 0, 0)), bt.Line((0.2, 0, 0), (0.5, 0.3, 0)), n=2.0)
+    t = np.array([1.0, 0.25, -0.5], np.float32)
+    root = bt.Op(B.OP_UNION, x, bt.Instance(x, transform=bt.Affine((1, 1, 1), (0, 0, 0, 1), tuple(t))))
+    _, tree = gui.compact_blobtree(root)
+    _, solo = gui.compact_blobtree(bt.Op(B.OP_UNION, x))
+    xyz = np.random.default_rng(4).uniform(-0.6, 0.9, size=(3000, 3)).astype(np.float32)
+    f_inst, _ = psgui.field_values(tree, xyz + t)
+    f_far, _ = psgui.field_values(solo, xyz + t)  # x's own field near the instance
+    f_x, _ = psgui.field_values(solo, xyz)
+    np.testing.assert_allclose(f_inst, np.maximum(f_x, f_far), atol=1e-5)
+    assert np.count_nonzero(f_x > 0.5) > 100
+
+
+def test_host_limits_of_pcm_and_instance():
+    """set_tree's checks (PSGUI_RET_UNSUPPORTED / PARAM_ERROR), on the host through
+    psgpu_gui_cull_boxes, and no generated kernels for these trees."""
+    from parsip_amd import gpu
+
+    def rc(root):
+        code, tree = gui.compact_blobtree(root)
+        assert code == 0
+        try:
+            gui.cull_boxes(tree)
+            return 1
+        except gpu.PsgpuError as e:
+            return e.code
+
+    pt = lambda x: bt.Point((x, 0, 0))  # noqa: E731
+    assert rc(_pcm_pair()) == 1
+    assert rc(bt.Op(B.OP_UNION, bt.Op(B.OP_PCM, pt(0), pt(0.3), pt(0.6)))) == gui.RET_UNSUPPORTED  # 3 kids
+    nested = gui.Pcm(gui.Pcm(pt(0), pt(0.3)), pt(0.6))
+    assert rc(bt.Op(B.OP_UNION, nested)) == gui.RET_UNSUPPORTED
+    x = bt.Op(B.OP_BLEND, pt(0), pt(0.3))
+    inner = bt.Op(B.OP_UNION, x, bt.Instance(x))
+    assert rc(bt.Op(B.OP_UNION, inner, bt.Instance(inner))) == gui.RET_UNSUPPORTED  # nested instancing
+    assert rc(bt.Op(B.OP_UNION, inner)) == 1
+    pcm_x = gui.Pcm(pt(0), pt(0.3))
+    assert rc(bt.Op(B.OP_UNION, pcm_x, gui.Pcm(pt(1), bt.Instance(pcm_x)))) == gui.RET_UNSUPPORTED
+    _, tree = gui.compact_blobtree(bt.Op(B.OP_UNION, bt.Instance(pt(5)), pt(0)))  # origin outside the tree
+    assert tree.prims["res1"][0][0] == -1.0
+    with pytest.raises(gpu.PsgpuError) as e:
+        gui.cull_boxes(tree)
+    assert e.value.code == -1  # PSGPU_RET_PARAM_ERROR
+    _, tree = gui.compact_blobtree(_pcm_pair())
+    with pytest.raises(RuntimeError, match="-7"):
+        gui.jit_compile(tree)
+
+
+PCM_SCENE = """[Global]
+NumLayers=1
+RootIDs=(0)
+[BLOBNODE 0]
+IsOperator=1
+OperatorType=UNION
+ChildrenCount=3
+ChildrenIDs=(1, 4, 5)
+[BLOBNODE 1]
+IsOperator=1
+OperatorType=PCM
+ChildrenCount=2
+ChildrenIDs=(2, 3)
+Propagate Left=0.3
+Propagate Right=0.25
+Attenuate Left=0.6
+Attenuate Right=0.8
+[BLOBNODE 2]
+IsOperator=0
+PrimitiveType=POINT
+position=(0.0, 0.0, 0.0)
+[BLOBNODE 3]
+IsOperator=0
+PrimitiveType=POINT
+position=(0.5, 0.05, 0.0)
+[BLOBNODE 4]
+IsOperator=0
+PrimitiveType=INSTANCE
+OriginalNodeIndex=1
+AffineTranslate=(1.5, 0.0, 0.0)
+[BLOBNODE 5]
+IsOperator=0
+PrimitiveType=INSTANCE
+OriginalNodeIndex=3
+AffineTranslate=(0.0, 1.0, 0.0)
+"""
+
+
+def test_scene_pcm_and_instance():
+    """The scene reader's PCM parameters (CPcm::loadScript) and INSTANCE origins
+    (OriginalNodeIndex, findNodeByID), through convert and the oracle."""
+    root = scene.load_scene(PCM_SCENE, from_text=True)[0]
+    pcm, inst_op, inst_prim = root.children
+    assert pcm.params == {"propagate_left": 0.3, "propagate_right": 0.25, "alpha_left": 0.6, "alpha_right": 0.8}
+    assert inst_op.params["origin"] is pcm and inst_prim.params["origin"] is pcm.children[1]
+    code, tree = gui.compact_blobtree(root)
+    assert code == 0
+    assert tree.prims["res1"][2].tolist() == [1.0, 1.0, 1.0, float(B.OP_PCM)]  # operator 1 (the root is 0)
+    assert tree.prims["res1"][3].tolist() == [1.0, 3.0, 0.0, float(B.PRIM_POINT)]
+    gui.cull_boxes(tree)  # the device's checks accept it
+    r = psgui.polygonize(tree, *tree.root_octree, 0.05, 0.5, threads=8)
+    assert r.info.ctTriangles > 0 and r.pcm_state[0] > 0.5
+    with pytest.raises(scene.SceneError):
+        scene.load_scene(PCM_SCENE.replace("OriginalNodeIndex=3", "OriginalNodeIndex=9"), from_text=True)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_random_ext_trees_run(seed):
+    code, tree = gui.compact_blobtree(random_ext_tree(seed))
+    assert code == 0
+    assert np.any(tree.ops["type"] == B.OP_PCM) and np.any(tree.prims["type"] == B.PRIM_INSTANCE)
+    r = psgui.polygonize(tree, *tree.root_octree, 0.1, 0.5, threads=8)
+    assert r.info.ctTriangles > 0 and np.all(np.isfinite(r.pos))
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 def test_jit_source_compiles_on_host(seed):
     """The generated compat kernels compile with hiprtc (no device needed)."""
@@ -263,7 +430,7 @@ def test_gpu_isovalue_and_empty_lattice(gui_ctx, train):
 
 @pytest.mark.gpu
 def test_gpu_rejects_unsupported_nodes(gui_ctx):
-    pcm = bt.Op(B.OP_PCM, bt.Point((0, 0, 0)), bt.Point((0.5, 0, 0)))
+    pcm = bt.Op(B.OP_PCM, bt.Point((0, 0, 0)), bt.Point((0.5, 0, 0)), bt.Point((0.9, 0, 0)))  # 3 kids
     code, tree = gui.compact_blobtree(pcm)
     assert code == 0
     from parsip_amd import gpu
@@ -324,5 +491,97 @@ def test_gpu_cull_toggle_between_set_tree_and_polygonize(order):
         p.set_tree(tree)  # the new setting now applies; still bit-exact
         gm, om = _both(p, tree, 0.06)
         assert_gui_mesh_equal(gm, om, f"cull toggled {order}, after set_tree")
+    finally:
+        p.close()
+
+
+# ---- PCM and Instance (the extended walk) ------------------------------------
+def _ext_ctx(jit):
+    from parsip_amd import gpu
+
+    gpu.load()
+    assert gpu.device_count() > 0, "no HIP device visible: GPU tests must run on an MI355X"
+    return gui.ParsipOptimized(0, jit=jit)
+
+
+def _ext_runs(p, tree, cs, runs=2):
+    """`runs` polygonizations in a row on the device and on the oracle, each reading the
+    contact state the previous one left: meshes, statistics and states bit-exact."""
+    lo, hi = tree.root_octree
+    p.setup(tree, (lo, hi), 0, cs, 0.5)
+    assert p.jit_status() == gui.JIT_NONE  # no generated kernels for these trees
+    state = np.array([0.5, 0.5], np.float32)
+    assert np.array_equal(p.pcm_state, state)
+    for k in range(runs):
+        p.run()
+        gm = p.exportMesh()
+        om = psgui.polygonize(tree, lo, hi, cs, 0.5, threads=8, pcm_state=state)
+        _info_equal(p.finish(), om.info)
+        assert_gui_mesh_equal(gm, om, f"run {k}")
+        state = om.pcm_state
+        assert np.array_equal(p.pcm_state, state), (k, p.pcm_state, state)
+    return state
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [0, 2])
+def test_gpu_pcm_contact_bit_exact(jit):
+    p = _ext_ctx(jit)
+    try:
+        _, tree = gui.compact_blobtree(_pcm_pair())
+        state = _ext_runs(p, tree, 0.04, runs=3)
+        assert state[0] > 0.5 and state[1] > 0.5
+        # a new set_tree (= convert) starts from ISO_VALUE again
+        p.set_tree(tree)
+        assert np.array_equal(p.pcm_state, np.array([0.5, 0.5], np.float32))
+    finally:
+        p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(1, 7))
+def test_gpu_random_ext_trees_bit_exact(seed):
+    p = _ext_ctx(2)
+    try:
+        code, tree = gui.compact_blobtree(random_ext_tree(seed))
+        assert code == 0
+        _ext_runs(p, tree, 0.07, runs=2)
+    finally:
+        p.close()
+
+
+@pytest.mark.gpu
+def test_gpu_ext_probe_reads_state():
+    p = _ext_ctx(0)
+    try:
+        _, tree = gui.compact_blobtree(random_ext_tree(4))
+        p.set_tree(tree)
+        xyz = np.random.default_rng(8).uniform(*tree.root_octree, size=(20000, 3)).astype(np.float32)
+        for state in ([0.5, 0.5], [0.93, 1.4]):
+            p.set_pcm_state(state)
+            gf, gc = p.field_values(xyz)
+            of, oc = psgui.field_values(tree, xyz, pcm_state=state)
+            assert np.array_equal(bits(gf), bits(of)) and np.array_equal(bits(gc), bits(oc)), state
+            assert np.array_equal(p.pcm_state, np.array(state, np.float32))  # probes leave it
+        assert np.count_nonzero(gf) > 1000
+    finally:
+        p.close()
+
+
+@pytest.mark.gpu
+def test_gpu_instance_scene_bit_exact():
+    """Instances of an operator and of a primitive beside their origins (and the colours
+    they take from them), under transforms."""
+    x = bt.Op(B.OP_RICCIBLEND, bt.Point((0, 0, 0), material=bt.Material(diffused=(1, 0, 0, 1))),
+              bt.Line((0.2, 0, 0), (0.5, 0.3, 0), material=bt.Material(diffused=(0, 1, 0, 1))), n=2.0)
+    y = bt.Cube((0, -0.6, 0), 0.15, material=bt.Material(diffused=(0, 0, 1, 1)))
+    root = bt.Op(B.OP_UNION, x, y,
+                 bt.Instance(x, transform=bt.Affine((1.2, 0.8, 1.0), (0.0, 0.0, 0.38268343, 0.9238795), (0.9, 0.3, 0))),
+                 bt.Op(B.OP_BLEND, bt.Instance(y, transform=bt.Affine((1, 1, 1), (0, 0, 0, 1), (0.5, -0.2, 0.1))),
+                       bt.Point((0.8, -0.6, 0.0))))
+    p = _ext_ctx(1)
+    try:
+        _, tree = gui.compact_blobtree(root)
+        _ext_runs(p, tree, 0.03, runs=1)
     finally:
         p.close()
