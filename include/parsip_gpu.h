@@ -254,7 +254,15 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        conservative field bounds and skips their S2 (default;
                                        output unchanged; JIT kernels only) */
 #define PSGPU_OPT_JIT           3   /* 0 interpreter, 1 specialised per structure (default),
-                                       2 specialised with parameters baked in */
+                                       2 specialised with parameters baked in (a recompile per
+                                       parameter change), 3 tiered: the structure kernels at once,
+                                       then -- once the model has stayed unchanged for
+                                       PSGPU_OPT_TIER_RUNS polygonizations -- its baked kernels,
+                                       compiled on a host thread and swapped in when loaded; a
+                                       set_model that changes the model returns to the structure
+                                       kernels at once (no compile on an animation's frame path).
+                                       Identical output in every mode */
+#define PSGPU_OPT_TIER_RUNS    18   /* tier-up threshold of PSGPU_OPT_JIT 3 (default 16, >= 1) */
 #define PSGPU_OPT_STAMPS       12   /* > 0: record a per-wave timeline for up to this many waves
                                        per kernel (psgpu_download_stamps); 0: off (default) */
 #define PSGPU_OPT_SPANS        13   /* > 0: the next this-many runs record each kernel's span on the
@@ -289,9 +297,12 @@ long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mat
 int  psgpu_jit_active(psgpu_ctx* ctx);
 /* 1 while the current model's specialised kernels are still compiling. */
 int  psgpu_jit_pending(psgpu_ctx* ctx);
-/* Block until the current model's compile has finished and adopt its kernels; returns
- * psgpu_jit_active afterwards (0: the compile failed and the interpreter stays). */
+/* Block until the current model's compile has finished and adopt its kernels (with
+ * PSGPU_OPT_JIT 3 also a baked compile already started); returns psgpu_jit_active
+ * afterwards (0: the compile failed and the interpreter stays). */
 int  psgpu_jit_wait(psgpu_ctx* ctx);
+/* The kernels the next run uses: 0 interpreter, 1 structure-specialised, 2 baked. */
+int  psgpu_jit_tier(psgpu_ctx* ctx);
 /* Generated specialised HIP source of the current model; returns its length. */
 int  psgpu_jit_source(psgpu_ctx* ctx, char* buf, size_t cap);
 

@@ -666,13 +666,58 @@ void jit_poll(psgpu_ctx* c, bool wait) {
         return;
     }
     if (!c->jit) fprintf(stderr, "psgpu: JIT unavailable, using the interpreter: %s\n", c->jitError.c_str());
+    c->tier = c->jit ? (c->useJit == 2 ? 2 : 1) : 0;
+}
+
+// PSGPU_OPT_JIT 3: adopt the baked kernels once their compile has finished (wait: block).
+void tier_poll(psgpu_ctx* c, bool wait) {
+    if (!c->tier2Pending) return;
+    if (!wait && c->tier2Fut.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return;
+    std::shared_ptr<const JitCode> code = c->tier2Fut.get();
+    c->tier2Pending = false;
+    c->tier2Fut = JitFuture();
+    std::string err;
+    std::shared_ptr<JitKernels> k = jit_load(*code, c->device, &err);
+    if (!k) {  // the structure kernels keep serving this model
+        c->tier2Failed = true;
+        fprintf(stderr, "psgpu: baked kernels unavailable, the structure kernels stay: %s\n", err.c_str());
+        return;
+    }
+    if (c->pending && c->useGraph) (void)hipStreamSynchronize(c->runStream);  // no graph dies in flight
+    drop_graphs(c);  // modules live as long as the process: in-flight runs keep theirs
+    c->jit1 = c->jit;
+    c->jit = k;
+    c->tier = 2;
+}
+
+// PSGPU_OPT_JIT 3: count a run of the unchanged model on the structure kernels and start the
+// baked compile at the threshold.
+void tier_count(psgpu_ctx* c) {
+    if (c->useJit != 3 || c->tier != 1 || c->tier2Pending || c->tier2Failed) return;
+    if (++c->staticRuns < c->tierRuns) return;
+    c->tier2Fut = jit_request(c->model, true, true, c->treeSplit != 0);
+    c->tier2Pending = true;
 }
 
 // Start (or restart) the compile of the current model's kernels.
 void jit_start(psgpu_ctx* c) {
     c->jit.reset();
+    c->jit1.reset();
     c->jitPending = false;
     c->jitFut = JitFuture();
+    c->tier = 0;
+    c->staticRuns = 0;
+    c->tier2Failed = false;
+    if (c->tier2Pending) c->retired.push_back(c->tier2Fut);  // finishes in the background
+    c->tier2Pending = false;
+    c->tier2Fut = JitFuture();
+    for (size_t i = 0; i < c->retired.size();) {  // forget the finished ones
+        if (c->retired[i].wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+            c->retired.erase(c->retired.begin() + (long)i);
+        } else {
+            ++i;
+        }
+    }
     if (!c->useJit || !c->haveModel) return;
     c->jitFut = jit_request(c->model, c->useJit == 2, true, c->treeSplit != 0);
     c->jitPending = true;
@@ -905,7 +950,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     const char* cullEnv = getenv("PSGPU_CULL");
     if (cullEnv) c->cull = atoi(cullEnv) != 0;
     const char* jitEnv = getenv("PSGPU_JIT");
-    if (jitEnv) c->useJit = std::min(2, std::max(0, atoi(jitEnv)));
+    if (jitEnv) c->useJit = std::min(3, std::max(0, atoi(jitEnv)));
     const char* asyncEnv = getenv("PSGPU_JIT_ASYNC");
     if (asyncEnv) c->jitAsync = atoi(asyncEnv) != 0;
     *out = c;
@@ -920,8 +965,13 @@ void psgpu_destroy(psgpu_ctx* c) {
     // an in-flight hiprtc compile must not outlive its owner: a process that exits while
     // LLVM compiles on the job thread tears LLVM's statics down under it
     if (c->jitPending && c->jitFut.valid()) c->jitFut.wait();
+    if (c->tier2Pending && c->tier2Fut.valid()) c->tier2Fut.wait();
+    for (JitFuture& f : c->retired)
+        if (f.valid()) f.wait();
     c->jitFut = JitFuture();
+    c->tier2Fut = JitFuture();
     c->jit.reset();
+    c->jit1.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans};
     for (void* b : bufs)
@@ -974,8 +1024,9 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         }
     }
     else if (option == PSGPU_OPT_SPLIT_MAX_QUEUED && value >= 0 && value <= 0xffffffffll) c->splitMaxQueued = (uint32_t)value;
+    else if (option == PSGPU_OPT_TIER_RUNS && value >= 1 && value <= (1 << 30)) c->tierRuns = (int)value;
     else if (option == PSGPU_OPT_JIT) {
-        if (value < 0 || value > 2) return PSGPU_RET_PARAM_ERROR;
+        if (value < 0 || value > 3) return PSGPU_RET_PARAM_ERROR;
         c->useJit = (int)value;
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
         drop_graphs(c);
@@ -1025,7 +1076,10 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     if (rc != PSGPU_RET_SUCCESS) { delete m; return rc; }
     if (c->pending) (void)hipStreamSynchronize(c->runStream);
     // captured graphs stay valid: specialised modules live as long as the process
-    // (jit_get's cache) and the replay key compares the kernels and every parameter
+    // (jit_get's cache) and the replay key compares the kernels and every parameter.
+    // The same model again (build_device_model zeroes every byte first) keeps its kernels,
+    // and with PSGPU_OPT_JIT 3 its tier and run count.
+    const bool same = c->haveModel && memcmp(&c->model, m, sizeof(DevModel)) == 0;
     c->model = *m;
     delete m;
     c->splittable = jit_splittable(c->model);
@@ -1033,7 +1087,7 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
     PSGPU_CHECK(hipStreamSynchronize(c->stream));
     c->haveModel = true;
-    jit_start(c);
+    if (!same || (!c->jit && !c->jitPending)) jit_start(c);
     return PSGPU_RET_SUCCESS;
 }
 
@@ -1062,6 +1116,8 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     c->mpuBegin = begin;
     c->mpuCount = end - begin;
     jit_poll(c, false);
+    tier_poll(c, false);
+    tier_count(c);
     // capacity from the largest finished run + 1/4 (grows only; finish() still re-runs
     // on an overflow, so a prediction that falls short costs time, never output)
     c->vcap = std::max(c->vcap, c->seenV + c->seenV / 4);
@@ -1416,14 +1472,26 @@ int psgpu_jit_pending(psgpu_ctx* c) {
 
 int psgpu_jit_wait(psgpu_ctx* c) {
     if (!c) return 0;
-    if (c->jitPending && set_device(c) == PSGPU_RET_SUCCESS) jit_poll(c, true);
+    if ((c->jitPending || c->tier2Pending) && set_device(c) == PSGPU_RET_SUCCESS) {
+        jit_poll(c, true);
+        tier_poll(c, true);
+    }
     return c->jit ? 1 : 0;
+}
+
+int psgpu_jit_tier(psgpu_ctx* c) {
+    if (!c) return 0;
+    if ((c->jitPending || c->tier2Pending) && set_device(c) == PSGPU_RET_SUCCESS) {
+        jit_poll(c, false);
+        tier_poll(c, false);
+    }
+    return c->tier;
 }
 
 // Generated specialised source for the current model (NUL-terminated, truncated to cap).
 int psgpu_jit_source(psgpu_ctx* c, char* buf, size_t cap) {
     if (!c || !c->haveModel) return PSGPU_RET_PARAM_ERROR;
-    const std::string s = jit_source(c->model, c->useJit == 2, c->treeSplit != 0);
+    const std::string s = jit_source(c->model, c->tier == 2 || c->useJit == 2, c->treeSplit != 0);
     if (buf && cap) {
         const size_t n = std::min(cap - 1, s.size());
         memcpy(buf, s.data(), n);

@@ -39,6 +39,16 @@ struct psgpu_ctx {
     JitFuture jitFut;                  // the current model's compile, while jitPending
     bool jitPending = false;
     std::string jitError;
+    // PSGPU_OPT_JIT 3 (tiered): once the model has stayed unchanged for tierRuns runs, its
+    // baked kernels compile on a host thread and replace the structure kernels (kept in jit1)
+    int tier = 0;                      // what `jit` holds: 0 none, 1 structure, 2 baked kernels
+    int tierRuns = 16;
+    int staticRuns = 0;                // runs of the current model on the structure kernels
+    JitFuture tier2Fut;                // the baked compile, while tier2Pending
+    bool tier2Pending = false;
+    bool tier2Failed = false;          // the baked compile failed: stay on tier 1 for this model
+    std::shared_ptr<JitKernels> jit1;  // the structure kernels while tier 2 serves
+    std::vector<JitFuture> retired;    // baked compiles of models since replaced (destroy waits)
     bool haveModel = false;
     int cull = 1;
     int debug = 0;

@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_set_model", "psgpu_polygonize", "psgpu_finish", "psgpu_mesh_device", "psgpu_download_mesh",
     "psgpu_download_stats", "psgpu_export_polympus", "psgpu_polygonize_mpus", "psgpu_last_kernel_times",
     "psgpu_field_values", "psgpu_set_option", "psgpu_jit_active", "psgpu_jit_source", "psgpu_jit_compile",
-    "psgpu_jit_pending", "psgpu_jit_wait", "psgpu_mpu_costs", "psgpu_split_costs",
+    "psgpu_jit_pending", "psgpu_jit_wait", "psgpu_jit_tier", "psgpu_mpu_costs", "psgpu_split_costs",
     "psgpu_group_create", "psgpu_group_destroy", "psgpu_group_size", "psgpu_group_context",
     "psgpu_group_set_option", "psgpu_group_set_model", "psgpu_group_jit_wait", "psgpu_group_set_split",
     "psgpu_group_get_split", "psgpu_group_polygonize", "psgpu_group_finish", "psgpu_group_download_mesh",
@@ -80,6 +80,8 @@ OPT_FINISH_QUAD = 14
 OPT_VERTEX_WIDE = 15
 OPT_TREE_SPLIT = 16
 OPT_SPLIT_MAX_QUEUED = 17
+OPT_TIER_RUNS = 18
+JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values
 STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
 BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3
@@ -120,6 +122,7 @@ def load(build_if_missing: bool = True):
         "psgpu_jit_active": ([vp], i32),
         "psgpu_jit_pending": ([vp], i32),
         "psgpu_jit_wait": ([vp], i32),
+        "psgpu_jit_tier": ([vp], i32),
         "psgpu_jit_source": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "psgpu_jit_compile": ([vp, vp, vp, i32, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_long),
         "psgpu_mpu_costs": ([vp, vp], i32),
@@ -308,6 +311,11 @@ class Polygonizer:
         """Block until the model's specialised kernels are compiled; True if they run."""
         return bool(self._L.psgpu_jit_wait(self._ctx))
 
+    @property
+    def jit_tier(self) -> int:
+        """The kernels the next run uses: 0 interpreter, 1 structure-specialised, 2 baked."""
+        return int(self._L.psgpu_jit_tier(self._ctx))
+
     def set_model(self, model: soa.Model, wait_jit: bool = True) -> None:
         """Upload a model.  The library compiles its specialised kernels on a host thread
         and serves polygonizations from the interpreter meanwhile (bit-identical output);
@@ -473,6 +481,16 @@ class Group:
         _check(self._L.psgpu_group_set_model(self._g, *model.ptrs()), "psgpu_group_set_model")
         if wait_jit:
             self._L.psgpu_group_jit_wait(self._g)
+
+    def jit_wait(self) -> bool:
+        """Block until every part's specialised kernels (and a started baked compile) are in place."""
+        return bool(self._L.psgpu_group_jit_wait(self._g))
+
+    @property
+    def jit_tier(self) -> int:
+        """The lowest tier the parts' next runs use (0 interpreter, 1 structure, 2 baked)."""
+        L = self._L
+        return min(int(L.psgpu_jit_tier(L.psgpu_group_context(self._g, i))) for i in range(self.n))
 
     def set_split(self, bounds) -> None:
         b = np.ascontiguousarray(bounds, np.uint32)

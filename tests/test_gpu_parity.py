@@ -374,3 +374,34 @@ def test_animation_driver(gpu_poly, oracle):
     model, cs, _ = synth.make_config("C2", frame=2)
     om = oracle.polygonize(model, cs, threads=8)
     assert seen[2][1] == len(om.pos)
+
+
+def test_tiered_kernels(oracle):
+    """PSGPU_OPT_JIT 3: the structure kernels serve at once; once the model has stayed unchanged
+    for OPT_TIER_RUNS runs the baked kernels take over (bit-exact); an animation frame (new
+    parameters, same structure) is back on the structure kernels at its first run, without
+    waiting for a compile; the same model again keeps the baked tier."""
+    p = gpu.Polygonizer(0)
+    try:
+        p.set_option(gpu.OPT_JIT, gpu.JIT_TIERED)
+        p.set_option(gpu.OPT_TIER_RUNS, 3)
+        model, cs, _ = synth.make_config("C2")
+        om = oracle.polygonize(model, cs, threads=8)
+        p.set_model(model)
+        assert p.jit_tier == 1
+        for k in range(3):
+            p.run(cs)
+            assert_mesh_matches(p.download(), p.stats(), om)
+        p.jit_wait()  # the third run started the baked compile
+        assert p.jit_tier == 2
+        p.run(cs)
+        assert_mesh_matches(p.download(), p.stats(), om)
+        p.set_model(model)  # the same bytes: nothing to recompile, the tier stays
+        assert p.jit_tier == 2
+        frame, cs1, _ = synth.make_config("C2", frame=3)
+        p.set_model(frame, wait_jit=False)  # the structure kernels are loaded: no compile
+        assert p.jit_tier == 1 and not p.jit_pending
+        p.run(cs1)
+        assert_mesh_matches(p.download(), p.stats(), oracle.polygonize(frame, cs1, threads=8))
+    finally:
+        p.close()

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, a kernel-trace profile of the bench command, PMC
+# One GPU-box session: parity tests, smoke, a kernel-trace profile of the bench command (its
+# kernels pinned to the baked ones, --jit 2: the tier the default --jit 3 times), PMC
 # passes (FETCH_SIZE, WRITE_SIZE; instruction mix, stalls, occupancy), then the bench lines
 # (C3 headline, C5 frame).  Every GPU step has its own time limit; the first failure ends the
 # script.  Usage (from the repo root, on the box): bash tools/gpu_round.sh TAG [notests]
@@ -26,11 +27,11 @@ if [ "$2" != "notests" ]; then
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
   cat $OUT/smoke.log
 fi
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --no-cpu --no-extras > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu --no-extras --steps 5 --warmup 1 > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu --no-extras --steps 5 --warmup 1 > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --no-cpu --no-extras --jit 2 > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu --no-extras --steps 5 --warmup 1 --jit 2 > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu --no-extras --steps 5 --warmup 1 --jit 2 > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 1; }
 python3 tools/traffic.py $OUT > $OUT/traffic.json && cp $OUT/traffic.json profiles/${TAG}_traffic.json || exit 1
-bash tools/pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+bash tools/pmc.sh $TAG/pmc --jit 2 > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
 cp $OUT/pmc/pmc.json profiles/${TAG}_pmc.json || exit 1
 cp $OUT/kt/run_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
 cat $OUT/traffic.json
