@@ -329,3 +329,31 @@ def test_cpp_parsip_optimized_run_train(exe, tmp_path):
         at += V * width * 4
         assert np.array_equal(bits(got), bits(getattr(om, name))), name
     assert np.array_equal(np.frombuffer(raw[at:], np.uint32).reshape(-1, 3), om.tris)
+
+
+@pytest.mark.gpu
+def test_cpp_parsip_optimized_run_pcm_instance(exe, tmp_path):
+    """PS::CParsipOptimizedGpu over a tree with a PCM and Instances (C++ conversion, origins
+    resolved by node id) on the device, against the oracle on the Python conversion: the
+    same arrays (test_cpp_compact_tree_matches_python), so the same mesh, bit-exact."""
+    import psgui
+    from gui_util import bits
+    from parsip_amd import gui
+
+    root = gui_ext_tree()
+    bt.compute_octrees(root)
+    tree, mesh = tmp_path / "tree.txt", tmp_path / "mesh.bin"
+    write_tree(root, str(tree))
+    r = subprocess.run([exe, "gui-run", str(tree), "0.06", str(mesh)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(mesh, "rb").read()
+    V, T = (int(x) for x in np.frombuffer(raw[:8], np.uint32))
+    _, ct = gui.compact_blobtree(root)
+    om = psgui.polygonize(ct, *ct.root_octree, 0.06, 0.5, threads=8)
+    assert (V, T) == (om.info.ctVertices, om.info.ctTriangles) and V > 0
+    at = 8
+    for name, width in (("pos", 3), ("nrm", 3), ("col", 4)):
+        got = np.frombuffer(raw[at:at + V * width * 4], np.float32).reshape(-1, width)
+        at += V * width * 4
+        assert np.array_equal(bits(got), bits(getattr(om, name))), name
+    assert np.array_equal(np.frombuffer(raw[at:], np.uint32).reshape(-1, 3), om.tris)
