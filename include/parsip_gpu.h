@@ -271,12 +271,17 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        of lanes per vertex (16 per wave), 3 a pair of lanes (32 per
                                        wave), 2 (default) the fewest vertices per wave whose waves
                                        hold the last run's vertices in one pass of the persistent
-                                       grid (16 or 32; else 64: small rank shares); identical output */
+                                       grid (16 or 32; else 64: small rank shares), at most 32 for a
+                                       run enqueued while no other context of the process has a run
+                                       pending on the device (a blocking caller, one context queueing
+                                       its frames); identical output */
 #define PSGPU_OPT_VERTEX_WIDE  15   /* k_vertex layout: 0 a quad of lanes per vertex (16 per wave),
                                        1 one lane per vertex walking its 4 edge samples (64 per wave,
                                        specialised kernels only), 2 (default) 64 when the last run's
                                        vertices overfill one pass of the persistent grid at 16 per
-                                       wave, else 16; identical output */
+                                       wave and other contexts of the process have runs pending on
+                                       the device (contexts taking frames in turn), else 16;
+                                       identical output */
 #define PSGPU_OPT_TREE_SPLIT   16   /* 1: k_precheck and k_mpu walk the root's two subtrees in two
                                        waves per brick / MPU and combine them (specialised kernels,
                                        trees whose root is a binary op over two ops); 2: only for runs

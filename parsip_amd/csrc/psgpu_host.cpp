@@ -6,6 +6,7 @@
 // stream, and the exports back to the reference PolyMPUs layout.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <algorithm>
 #include <numeric>
 #include <cmath>
@@ -534,6 +535,8 @@ hipError_t launch_jit(hipFunction_t f, uint32_t blocks, uint32_t threads, size_t
 // the last run's vertices, 16 per wave, fit the persistent grid's waves in one pass (each
 // wave then walks a quarter of what a 64-vertex wave does), else a pair of lanes (32) when
 // they do 32 per wave, otherwise one lane per vertex (64: fewest waves in total).
+// A run alone on its device (c->alone) takes at most 32 per wave: the spans, not the total
+// work, set its time (C3 full grid, one engine: 0.1077 vs 0.1110 ms with the quad k_vertex).
 int finish_vpw(const psgpu_ctx* c) {
     if (c->finishQuad == 0) return 64;
     if (c->finishQuad == 1) return 16;
@@ -541,7 +544,7 @@ int finish_vpw(const psgpu_ctx* c) {
     const uint64_t waves = (uint64_t)c->numCUs * (uint64_t)c->finishBlocksPerCU * 4u;
     if (c->lastV == 0) return 64;
     if ((uint64_t)c->lastV <= 16u * waves) return 16;
-    if ((uint64_t)c->lastV <= 32u * waves) return 32;
+    if ((uint64_t)c->lastV <= 32u * waves || c->alone) return 32;
     return 64;
 }
 
@@ -554,7 +557,7 @@ int vertex_vpw(const psgpu_ctx* c) {
     if (!c->jit || c->vertexWide == 0) return 16;
     if (c->vertexWide == 1) return 64;
     const uint64_t waves = (uint64_t)c->numCUs * (uint64_t)c->vertexBlocksPerCU * 4u;
-    return (uint64_t)c->lastV > 16u * waves ? 64 : 16;
+    return (uint64_t)c->lastV > 16u * waves && !c->alone ? 64 : 16;  // a lone run: the quad
 }
 
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
@@ -644,6 +647,18 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     PSGPU_CHECK(hipGraphLaunch(g.exec, s));
     return PSGPU_RET_SUCCESS;
+}
+
+// Contexts with a run enqueued and not yet collected (psgpu_finish), per device, over the
+// process: a run enqueued while no other context has one pending on its device is alone on
+// it (a blocking caller, a frame-at-a-time editor, one context queueing its frames) and takes
+// the layouts with the shortest spans; runs that overlap other contexts' (contexts taking
+// frames in turn) take the layouts with the least total work.
+std::atomic<int> g_pendingRuns[64];
+void set_pending(psgpu_ctx* c, bool v) {
+    if (c->pending == v) return;
+    c->pending = v;
+    g_pendingRuns[c->device & 63].fetch_add(v ? 1 : -1);
 }
 
 // Adopt the model's specialised kernels once their compile has finished (wait: block for
@@ -961,6 +976,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    set_pending(c, false);
     drop_graphs(c);
     // an in-flight hiprtc compile must not outlive its owner: a process that exits while
     // LLVM compiles on the job thread tears LLVM's statics down under it
@@ -996,7 +1012,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         // restart the output / work-queue buffers at this vertex capacity (they grow on demand);
         // a pending result is dropped with them
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
-        c->pending = false;
+        set_pending(c, false);
         c->seenV = c->seenT = c->seenShardV = c->seenShardT = 0;
         void* bufs[] = {c->vk, c->vp, c->tq, c->pos, c->nrm, c->col, c->tris};
         for (void* b : bufs)
@@ -1126,10 +1142,13 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     c->tShardCap = std::max(c->tShardCap, c->seenShardT + c->seenShardT / 4);
     rc = ensure_buffers(c, c->mpuCount);
     if (rc != PSGPU_RET_SUCCESS) return rc;
+    // alone: no OTHER context has a run pending on the device (this context's own earlier
+    // runs share its stream, so they never overlap this one)
+    c->alone = g_pendingRuns[c->device & 63].load() - (c->pending ? 1 : 0) == 0;
     rc = enqueue(c, s);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     c->runStream = s;
-    c->pending = true;
+    set_pending(c, true);
     c->haveResult = false;
     return PSGPU_RET_SUCCESS;
 }
@@ -1140,7 +1159,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         int rc = set_device(c);
         if (rc != PSGPU_RET_SUCCESS) return rc;
         PSGPU_CHECK(hipStreamSynchronize(c->runStream));
-        c->pending = false;
+        set_pending(c, false);
         // grow and re-run if the work queues or the compact outputs did not fit
         for (int attempt = 0; attempt < 4; ++attempt) {
             const DevCounters& h = *c->hostCtr;

@@ -39,6 +39,9 @@ struct psgpu_ctx {
     JitFuture jitFut;                  // the current model's compile, while jitPending
     bool jitPending = false;
     std::string jitError;
+    // this run enqueued while no other run of the process was pending on the device (a
+    // blocking caller): the layout defaults pick the shorter-span (latency) layouts
+    bool alone = false;
     // PSGPU_OPT_JIT 3 (tiered): once the model has stayed unchanged for tierRuns runs, its
     // baked kernels compile on a host thread and replace the structure kernels (kept in jit1)
     int tier = 0;                      // what `jit` holds: 0 none, 1 structure, 2 baked kernels
