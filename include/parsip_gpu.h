@@ -199,7 +199,9 @@ int  psgpu_device_count(void);
 int  psgpu_set_model(psgpu_ctx* ctx, const PsSoaBlobPrims* prims,
                      const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops);
 /* Enqueue a polygonization of global MPUs [mpuBegin, mpuEnd) (clamped to the
- * lattice; pass 0, UINT32_MAX for all) on `stream` (hipStream_t or NULL). Async. */
+ * lattice; pass 0, UINT32_MAX for all) on `stream` (hipStream_t or NULL). Async.
+ * A range (after clamping) holds fewer than 2^26 MPUs (a 4096^3-cell lattice is 2^27:
+ * split it into ranges); a larger one returns PSGPU_RET_PARAM_ERROR. */
 int  psgpu_polygonize(psgpu_ctx* ctx, float cellsize, uint32_t mpuBegin, uint32_t mpuEnd,
                       void* stream);
 /* Wait for the last polygonize and report counts / errors.  If the output

@@ -1140,7 +1140,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
             const uint32_t shard = d & (kShards - 1);
             if (lane == 0) {
                 sQ[0] = atomicAdd(&p.ctr->shard[shard].v, V);
-                sQ[1] = atomicAdd(&p.ctr->shard[shard].t, T);
+                sQ[1] = atomicAdd(&p.ctr->shard[w & (kShards - 1)].t, T);  // TriRec: shard = w & 63
                 p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
                 if (T > 0) atomicAdd(&p.ctr->shard[shard].s, 1u);
                 if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
@@ -1152,7 +1152,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     const bool recs = work && !(p.debug & 2u);  // ablation bit 1: pass 1 only
     const uint32_t shard = d & (kShards - 1);
     VertexKey* vk = p.vk + (size_t)shard * p.vShardCap;
-    TriRec* tq = p.tq + (size_t)shard * p.tShardCap;
+    TriRec* tq = p.tq + (size_t)(w & (kShards - 1)) * p.tShardCap;
 
     // pass 2 (:703-762), one lane per new vertex r (batches of 64 dealt to the MPU's waves
     // in turn): its cell is the last cell whose first vertex id is <= r; it is that cell's
@@ -1211,7 +1211,8 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
                 v[sv] = edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax];
             }
             const uint32_t g = qt + r;
-            if (g < p.tShardCap) tq[g] = TriRec{w, r | (v[0] << 11) | ((v[1] & 1023u) << 22), (v[1] >> 10) | (v[2] << 1)};
+            if (g < p.tShardCap)
+                tq[g] = TriRec{r | ((v[2] >> 10) << 11) | ((w >> 6) << 12), v[0] | (v[1] << 11) | ((v[2] & 1023u) << 22)};
         }
     }
 }
@@ -1438,6 +1439,41 @@ __device__ __forceinline__ CullMask cull_mask_mpus(const Params& p, uint32_t w) 
     return cm;
 }
 
+// The edge of a vertex record (PS_Polygonizer.cpp:722-724): e1 = lo + cs*s, e2 = e1 with
+// e2[axis] += cs, d = e2 - e1, and its samples e1 + d * (l/3), l = 0..3 (:744-755).  k_vertex
+// brackets the root with them; k_finish recomputes the root from the record (iv, scale)
+// through the same expressions, so both kernels see the same bits.
+struct EdgeSeg {
+    float e[3], d[3];
+};
+__device__ __forceinline__ EdgeSeg edge_segment(const Params& p, uint32_t w, uint32_t key) {
+    float o[3];
+    mpu_origin(p, w + p.mpuBegin, o);  // the MPU origin, as k_mpu computed it
+    const int sx = key & 7, sy = (key >> 3) & 7, sz = (key >> 6) & 7, ax = (key >> 9) & 3;
+    const float cs = p.cs;
+    EdgeSeg E;
+    E.e[0] = o[0] + cs * (float)sx;
+    E.e[1] = o[1] + cs * (float)sy;
+    E.e[2] = o[2] + cs * (float)sz;
+    E.d[0] = (ax == 0 ? E.e[0] + cs : E.e[0]) - E.e[0];
+    E.d[1] = (ax == 1 ? E.e[1] + cs : E.e[1]) - E.e[1];
+    E.d[2] = (ax == 2 ? E.e[2] + cs : E.e[2]) - E.e[2];
+    return E;
+}
+__device__ __forceinline__ float edge_sample(float e, float d, int l) {
+    const float third = 1.0f / 3.0f;
+    return e + d * ((float)l * third);
+}
+// the linear root on [sample iv - 1, sample iv] (:756-762): a + scale * (b - a)
+__device__ __forceinline__ void vertex_root(const EdgeSeg& E, uint32_t iv, float scale, float pos[3]) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float a = edge_sample(E.e[c], E.d[c], (int)iv - 1);
+        const float b = edge_sample(E.e[c], E.d[c], (int)iv);
+        pos[c] = a + scale * (b - a);
+    }
+}
+
 #ifndef PSGPU_V_N
 #define PSGPU_V_N 1  // vertices per quad of lanes per k_vertex pass (2: bigger culling boxes, slower)
 #endif
@@ -1454,10 +1490,7 @@ __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
-    const float third = 1.0f / 3.0f;
     const int j = lane & 3;
-    const float r = (float)j * third;
-    const float cs = p.cs;
     if (blockIdx.x < p.scanBlocks) scan_counts_block(p, blockIdx.x);  // block-uniform
     __shared__ uint32_t sCnt[kShards];
     stage_shard_counts(p, 1, sCnt);  // ShardCtr::v
@@ -1477,23 +1510,13 @@ if constexpr (VPW == 64) {
         if (!valid) rr = first;
         const size_t rec = (size_t)shard * p.vShardCap + rr;
         const VertexKey R = p.vk[rec];
-        float o[3];
-        mpu_origin(p, R.w + p.mpuBegin, o);
-        const uint32_t key = R.vidKey >> 16;
-        const int sx = key & 7, sy = (key >> 3) & 7, sz = (key >> 6) & 7, ax = (key >> 9) & 3;
-        const float e1x = o[0] + cs * (float)sx;
-        const float e1y = o[1] + cs * (float)sy;
-        const float e1z = o[2] + cs * (float)sz;
-        const float dX = (ax == 0 ? e1x + cs : e1x) - e1x;
-        const float dY = (ax == 1 ? e1y + cs : e1y) - e1y;
-        const float dZ = (ax == 2 ? e1z + cs : e1z) - e1z;
+        const EdgeSeg E = edge_segment(p, R.w, R.vidKey >> 16);
         float xs[4], ys[4], zs[4], fs[4];
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
-            const float rs = (float)s2 * third;
-            xs[s2] = e1x + dX * rs;
-            ys[s2] = e1y + dY * rs;
-            zs[s2] = e1z + dZ * rs;
+            xs[s2] = edge_sample(E.e[0], E.d[0], s2);
+            ys[s2] = edge_sample(E.e[1], E.d[1], s2);
+            zs[s2] = edge_sample(E.e[2], E.d[2], s2);
         }
         CullMask cm{0ull, 0ull};
         if (p.cull) cm = cull_mask_mpus(p, R.w);
@@ -1503,20 +1526,13 @@ if constexpr (VPW == 64) {
         } else {
             ev.template evaln<0, false, 4>(xs, ys, zs, cm, fs, nullptr);
         }
+        // first sample whose inside state differs from sample 0, else 3 (:744-755); the
+        // root itself is k_finish's (vertex_root)
         const bool st0 = fs[0] >= 0.5f;
         const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
         const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
         const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
-        const float ax0 = iv == 1 ? xs[0] : (iv == 2 ? xs[1] : xs[2]);
-        const float ay0 = iv == 1 ? ys[0] : (iv == 2 ? ys[1] : ys[2]);
-        const float az0 = iv == 1 ? zs[0] : (iv == 2 ? zs[1] : zs[2]);
-        const float bx0 = iv == 1 ? xs[1] : (iv == 2 ? xs[2] : xs[3]);
-        const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
-        const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
-        const float scale = (0.5f - fa) / (fb - fa);
-        if (valid)
-            p.vp[rec] = VertexPos{{ax0 + scale * (bx0 - ax0), ay0 + scale * (by0 - ay0), az0 + scale * (bz0 - az0)},
-                                  (scale >= 0.0f && scale <= 1.0f) ? 1.0f : 0.0f};
+        if (valid) p.vp[rec] = VertexPos{(0.5f - fa) / (fb - fa), (uint32_t)iv};
     }
 } else {
     const ShardBatches sb(sCnt, p.vShardCap, 16 * VN);
@@ -1525,8 +1541,8 @@ if constexpr (VPW == 64) {
         sb.locate(batch, &shard, &first, &count);
         bool valid[VN];
         size_t rec[VN];
-        float e1x[VN], e1y[VN], e1z[VN], dX[VN], dY[VN], dZ[VN], qx[VN], qy[VN], qz[VN];
-        uint32_t key[VN], wrec[VN];
+        float qx[VN], qy[VN], qz[VN];
+        uint32_t wrec[VN];
 #pragma unroll
         for (int n = 0; n < VN; ++n) {
             uint32_t rr = first + ((uint32_t)lane >> 2) + 16u * (uint32_t)n;
@@ -1534,24 +1550,11 @@ if constexpr (VPW == 64) {
             if (!valid[n]) rr = first;
             rec[n] = (size_t)shard * p.vShardCap + rr;
             const VertexKey R = p.vk[rec[n]];
-            float o[3];
-            mpu_origin(p, R.w + p.mpuBegin, o);  // the MPU origin, as k_mpu computed it
             wrec[n] = R.w;
-            key[n] = R.vidKey >> 16;
-            const int sx = key[n] & 7, sy = (key[n] >> 3) & 7, sz = (key[n] >> 6) & 7, ax = (key[n] >> 9) & 3;
-            // e1 = lo + cs*s, e2 = e1 with e2[axis] += cs (:722-724)
-            e1x[n] = o[0] + cs * (float)sx;
-            e1y[n] = o[1] + cs * (float)sy;
-            e1z[n] = o[2] + cs * (float)sz;
-            const float e2x = ax == 0 ? e1x[n] + cs : e1x[n];
-            const float e2y = ax == 1 ? e1y[n] + cs : e1y[n];
-            const float e2z = ax == 2 ? e1z[n] + cs : e1z[n];
-            dX[n] = e2x - e1x[n];
-            dY[n] = e2y - e1y[n];
-            dZ[n] = e2z - e1z[n];
-            qx[n] = e1x[n] + dX[n] * r;
-            qy[n] = e1y[n] + dY[n] * r;
-            qz[n] = e1z[n] + dZ[n] * r;
+            const EdgeSeg E = edge_segment(p, R.w, R.vidKey >> 16);
+            qx[n] = edge_sample(E.e[0], E.d[0], j);  // lane j of the quad: sample j
+            qy[n] = edge_sample(E.e[1], E.d[1], j);
+            qz[n] = edge_sample(E.e[2], E.d[2], j);
         }
         // every edge sample lies in its MPU's box (k_mpu's mask; the d^2 >= 1.02 margin
         // absorbs the last-bit rounding of e1 + cs vs lo + 7 cs)
@@ -1572,35 +1575,19 @@ if constexpr (VPW == 64) {
         }
 #pragma unroll
         for (int n = 0; n < VN; ++n) {
-            float fs[4], xs[4], ys[4], zs[4];
+            float fs[4];
             fs[0] = quad_bcast<0>(f[n]);
             fs[1] = quad_bcast<1>(f[n]);
             fs[2] = quad_bcast<2>(f[n]);
             fs[3] = quad_bcast<3>(f[n]);
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const float rs = (float)s2 * third;
-                xs[s2] = e1x[n] + dX[n] * rs;
-                ys[s2] = e1y[n] + dY[n] * rs;
-                zs[s2] = e1z[n] + dZ[n] * rs;
-            }
             // first sample whose inside state differs from sample 0, else 3 (:744-755)
             const bool st0 = fs[0] >= 0.5f;
             const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
             const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
             const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
-            const float ax0 = iv == 1 ? xs[0] : (iv == 2 ? xs[1] : xs[2]);
-            const float ay0 = iv == 1 ? ys[0] : (iv == 2 ? ys[1] : ys[2]);
-            const float az0 = iv == 1 ? zs[0] : (iv == 2 ? zs[1] : zs[2]);
-            const float bx0 = iv == 1 ? xs[1] : (iv == 2 ? xs[2] : xs[3]);
-            const float by0 = iv == 1 ? ys[1] : (iv == 2 ? ys[2] : ys[3]);
-            const float bz0 = iv == 1 ? zs[1] : (iv == 2 ? zs[2] : zs[3]);
-            const float scale = (0.5f - fa) / (fb - fa);
-            if (valid[n] && j == 0) {  // into the record; k_finish adds normal and colour
-                // onSeg 1: p lies on its bracketing segment, inside the MPU box (no inf/NaN)
-                p.vp[rec[n]] = VertexPos{{ax0 + scale * (bx0 - ax0), ay0 + scale * (by0 - ay0), az0 + scale * (bz0 - az0)},
-                                         (scale >= 0.0f && scale <= 1.0f) ? 1.0f : 0.0f};
-            }
+            // into the record; k_finish recomputes the root there (vertex_root) and adds
+            // normal and colour
+            if (valid[n] && j == 0) p.vp[rec[n]] = VertexPos{(0.5f - fa) / (fb - fa), (uint32_t)iv};
         }
     }
 }
@@ -1608,7 +1595,7 @@ if constexpr (VPW == 64) {
 
 // Finish: per vertex fieldValueAndColor's value and colour walk (PS_Polygonizer.cpp:777-778,
 // 1378-1551) and the three normal samples (:780-781, 1598-1622), then the triangle records
-// -> global vertex ids.  Runs after k_vertex wrote the positions.  VPW 64: one lane per
+// -> global vertex ids.  Runs after k_vertex wrote the roots.  VPW 64: one lane per
 // vertex walking its 4 points; VPW 16: a quad of lanes per vertex, one point each (a
 // quarter of the walk per wave: shorter spans when the vertices do not fill the persistent
 // grid, e.g. a small rank share; more total work otherwise).  Same values either way.
@@ -1663,17 +1650,21 @@ if constexpr (VPW == 16) {
         const VertexKey K = p.vk[ri];
         const VertexPos R = p.vp[ri];
         const uint32_t gi = (uint32_t)p.offs[K.w] + (K.vidKey & 0xffffu);
+        float P[3];  // the root, recomputed from k_vertex's record with its expressions
+        vertex_root(edge_segment(p, K.w, K.vidKey >> 16), R.iv, R.scale, P);
+        // on its bracketing segment: inside the MPU box (no inf / NaN)
+        const bool onSeg = R.scale >= 0.0f && R.scale <= 1.0f;
         float c[3] = {0.0f, 0.0f, 0.0f};
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
         if (!(p.debug & 32u)) {  // ablation bit 5: no walks
             CullMask cm{0ull, 0ull};
             if (p.cull) {
-                if (ballot(!(R.onSeg == 1.0f)) == 0ull) cm = cull_mask_mpus(p, K.w);
-                else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
+                if (ballot(!onSeg) == 0ull) cm = cull_mask_mpus(p, K.w);
+                else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
             }
-            const float qx = qj == 1 ? R.pos[0] + delta : R.pos[0];
-            const float qy = qj == 2 ? R.pos[1] + delta : R.pos[1];
-            const float qz = qj == 3 ? R.pos[2] + delta : R.pos[2];
+            const float qx = qj == 1 ? P[0] + delta : P[0];
+            const float qy = qj == 2 ? P[1] + delta : P[1];
+            const float qz = qj == 3 ? P[2] + delta : P[2];
             float c4[3];
             const float g = ev.template eval<1, true>(qx, qy, qz, cm, c4);
             c[0] = quad_bcast<0>(c4[0]);
@@ -1690,7 +1681,7 @@ if constexpr (VPW == 16) {
         }
         if (valid && qj < 3 && gi < p.vCap) {  // past vCap: finish() grows and re-runs
             const uint32_t o = gi * 3 + (uint32_t)qj;
-            p.pos[o] = qj == 0 ? R.pos[0] : (qj == 1 ? R.pos[1] : R.pos[2]);
+            p.pos[o] = qj == 0 ? P[0] : (qj == 1 ? P[1] : P[2]);
             p.nrm[o] = qj == 0 ? nx : (qj == 1 ? ny : nz);
             p.col[o] = qj == 0 ? c[0] : (qj == 1 ? c[1] : c[2]);
         }
@@ -1711,18 +1702,22 @@ if constexpr (VPW == 16) {
         const VertexKey K = p.vk[ri];
         const VertexPos R = p.vp[ri];
         const uint32_t gi = (uint32_t)p.offs[K.w] + (K.vidKey & 0xffffu);
+        float P[3];  // the root, recomputed from k_vertex's record with its expressions
+        vertex_root(edge_segment(p, K.w, K.vidKey >> 16), R.iv, R.scale, P);
+        // on its bracketing segment: inside the MPU box (no inf / NaN)
+        const bool onSeg = R.scale >= 0.0f && R.scale <= 1.0f;
         float c[3] = {0.0f, 0.0f, 0.0f};
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
         if (!(p.debug & 32u)) {  // ablation bit 5: no walks
             CullMask cm{0ull, 0ull};
             if (p.cull) {
-                if (ballot(!(R.onSeg == 1.0f)) == 0ull) cm = cull_mask_mpus(p, K.w);
-                else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
+                if (ballot(!onSeg) == 0ull) cm = cull_mask_mpus(p, K.w);
+                else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
             }
             // lane 0: p, p + delta e_x; lane 1: p + delta e_y, p + delta e_z
-            const float qx[2] = {R.pos[0], pj == 0 ? R.pos[0] + delta : R.pos[0]};
-            const float qy[2] = {pj == 1 ? R.pos[1] + delta : R.pos[1], R.pos[1]};
-            const float qz[2] = {R.pos[2], pj == 1 ? R.pos[2] + delta : R.pos[2]};
+            const float qx[2] = {P[0], pj == 0 ? P[0] + delta : P[0]};
+            const float qy[2] = {pj == 1 ? P[1] + delta : P[1], P[1]};
+            const float qz[2] = {P[2], pj == 1 ? P[2] + delta : P[2]};
             float g[2], c6[6];
             ev.template evaln<1, true, 2>(qx, qy, qz, cm, g, c6);
             const float o0 = PSGPU_DPP_F(g[0], 0xB1), o1 = PSGPU_DPP_F(g[1], 0xB1);
@@ -1745,11 +1740,11 @@ if constexpr (VPW == 16) {
         }
         if (valid && gi < p.vCap) {  // past vCap: finish() grows and re-runs
             const uint32_t o = gi * 3 + (uint32_t)pj;
-            p.pos[o] = pj == 0 ? R.pos[0] : R.pos[1];
+            p.pos[o] = pj == 0 ? P[0] : P[1];
             p.nrm[o] = pj == 0 ? nx : ny;
             p.col[o] = pj == 0 ? c[0] : c[1];
             if (pj == 0) {
-                p.pos[gi * 3 + 2] = R.pos[2];
+                p.pos[gi * 3 + 2] = P[2];
                 p.nrm[gi * 3 + 2] = nz;
                 p.col[gi * 3 + 2] = c[2];
             }
@@ -1767,6 +1762,10 @@ if constexpr (VPW == 16) {
         const VertexKey K = p.vk[ri];
         const VertexPos R = p.vp[ri];
         const uint32_t gi = (uint32_t)p.offs[K.w] + (K.vidKey & 0xffffu);
+        float P[3];  // the root, recomputed from k_vertex's record with its expressions
+        vertex_root(edge_segment(p, K.w, K.vidKey >> 16), R.iv, R.scale, P);
+        // on its bracketing segment: inside the MPU box (no inf / NaN)
+        const bool onSeg = R.scale >= 0.0f && R.scale <= 1.0f;
         float c[3] = {0.0f, 0.0f, 0.0f};
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
         if (!(p.debug & 32u)) {  // ablation bit 5: no walks
@@ -1774,15 +1773,15 @@ if constexpr (VPW == 16) {
             // every normal sample; otherwise the wave's own box grown by delta
             CullMask cm{0ull, 0ull};
             if (p.cull) {
-                if (ballot(!(R.onSeg == 1.0f)) == 0ull) cm = cull_mask_mpus(p, K.w);
-                else cm = cull_mask_points(M, R.pos[0], R.pos[1], R.pos[2], true, delta);
+                if (ballot(!onSeg) == 0ull) cm = cull_mask_mpus(p, K.w);
+                else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
             }
             // value + colour at p and the normal's per-point fieldValue at p + delta*e_a
             // (:1598-1622) as four points of one walk (the colour of points 1-3 is dead
             // code); then SimdNormalize (rsqrt -> IEEE 1/sqrtf)
-            const float qx[4] = {R.pos[0], R.pos[0] + delta, R.pos[0], R.pos[0]};
-            const float qy[4] = {R.pos[1], R.pos[1], R.pos[1] + delta, R.pos[1]};
-            const float qz[4] = {R.pos[2], R.pos[2], R.pos[2], R.pos[2] + delta};
+            const float qx[4] = {P[0], P[0] + delta, P[0], P[0]};
+            const float qy[4] = {P[1], P[1], P[1] + delta, P[1]};
+            const float qz[4] = {P[2], P[2], P[2], P[2] + delta};
             float g[4], c4[12];
             ev.template evaln<1, true, 4>(qx, qy, qz, cm, g, c4);
             c[0] = c4[0];
@@ -1798,9 +1797,9 @@ if constexpr (VPW == 16) {
             nz = nz * im;
         }
         if (valid && gi < p.vCap) {  // past vCap: finish() grows and re-runs
-            p.pos[gi * 3 + 0] = R.pos[0];
-            p.pos[gi * 3 + 1] = R.pos[1];
-            p.pos[gi * 3 + 2] = R.pos[2];
+            p.pos[gi * 3 + 0] = P[0];
+            p.pos[gi * 3 + 1] = P[1];
+            p.pos[gi * 3 + 2] = P[2];
             p.nrm[gi * 3 + 0] = nx;
             p.nrm[gi * 3 + 1] = ny;
             p.nrm[gi * 3 + 2] = nz;
@@ -1818,13 +1817,13 @@ if constexpr (VPW == 16) {
         const uint32_t t = first + lane;
         if (t >= count) continue;
         const TriRec R = p.tq[(size_t)shard * p.tShardCap + t];
-        const uint64_t o = p.offs[R.w];
+        const uint64_t o = p.offs[((R.a >> 12) << 6) | shard];  // the record's shard is w & 63
         const uint32_t gt = (uint32_t)(o >> 32) + (R.a & 2047u);
         const uint32_t base = (uint32_t)o;
         if (gt >= p.tCap) continue;  // finish() grows and re-runs
-        p.tris[gt * 3 + 0] = base + ((R.a >> 11) & 2047u);
-        p.tris[gt * 3 + 1] = base + ((R.a >> 22) | ((R.b & 1u) << 10));
-        p.tris[gt * 3 + 2] = base + ((R.b >> 1) & 2047u);
+        p.tris[gt * 3 + 0] = base + (R.b & 2047u);
+        p.tris[gt * 3 + 1] = base + ((R.b >> 11) & 2047u);
+        p.tris[gt * 3 + 2] = base + ((R.b >> 22) | (((R.a >> 11) & 1u) << 10));
     }
 }
 

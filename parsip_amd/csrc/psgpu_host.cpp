@@ -1120,6 +1120,7 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     if (total > 0xffffffffull) return PSGPU_RET_PARAM_ERROR;
     const uint32_t end = (uint32_t)std::min<uint64_t>(mpuEnd, total);
     const uint32_t begin = std::min(mpuBegin, end);
+    if (end - begin >= kMaxRangeMpus) return PSGPU_RET_PARAM_ERROR;  // TriRec's 20-bit slot field
     if (begin != c->mpuBegin || end - begin != c->mpuCount || cellsize != c->lastCs) {
         // another range or lattice: the last run's survivor count says nothing about this
         // one -- size k_mpu for the whole range (no re-run) until a run of it finishes.  A new

@@ -142,20 +142,24 @@ struct DevModel {
 
 // Compact-mesh work records written by the MPU kernel.
 // A vertex record in two arrays, so that each kernel moves only what it uses: k_mpu writes
-// the key (8 B), k_vertex reads it and writes the position (16 B), k_finish reads both.
+// the key (8 B), k_vertex reads it and writes the root (8 B), k_finish reads both and
+// recomputes the position from them with k_vertex's own expressions (vertex_root).
 struct VertexKey {       // 8 B: MPU slot in the range, vid | edge key << 16
     uint32_t w;
     uint32_t vidKey;     // vid | key << 16, key = sx | sy<<3 | sz<<6 | axis<<9
 };
-struct VertexPos {       // 16 B (k_vertex): the root, and 1 if it lies on its bracketing segment
-    float pos[3];
-    float onSeg;
+struct VertexPos {       // 8 B (k_vertex): the linear root's scale on its bracketing segment
+    float scale;         // (0.5 - fa) / (fb - fa)
+    uint32_t iv;         // the segment [sample iv - 1, sample iv] of the edge's 4 samples (1..3)
 };
-struct TriRec {          // 12 B: MPU slot, then 11-bit fields (an MPU has at most 1,715
-    uint32_t w;          // triangles and 1,344 edges): tlocal | v0 << 11 | v1 << 22 (low 10
-    uint32_t a;          // bits), then v1 >> 10 | v2 << 1
-    uint32_t b;
+// Triangle record, 8 B.  An MPU has at most 1,715 triangles and 1,344 edges (11-bit local
+// ids); the record sits in queue shard w & 63 of its MPU slot w, so the slot needs only
+// w >> 6 (20 bits: ranges of up to 2^26 MPUs, checked by psgpu_polygonize).
+struct TriRec {
+    uint32_t a;          // tlocal | (v2 >> 10) << 11 | (w >> 6) << 12
+    uint32_t b;          // v0 | v1 << 11 | (v2 & 1023) << 22
 };
+constexpr uint32_t kMaxRangeMpus = 1u << 26;
 
 // Device-side scalars of one polygonization.
 // Work records are appended to kShards independent queues so that no single counter
@@ -222,7 +226,7 @@ struct Params {
     uint32_t scanBlocks;    // offsets-scan blocks (the first blocks of k_vertex)
     uint32_t scanChunks;    // kScanItems chunks per scan block
     VertexKey* vk;          // kShards queues of vShardCap vertex records (keys ...
-    VertexPos* vp;          // ... and positions, same indexing)
+    VertexPos* vp;          // ... and roots, same indexing)
     uint32_t vShardCap;
     TriRec* tq;             // kShards queues of tShardCap records
     uint32_t tShardCap;

@@ -28,6 +28,8 @@ _LIB = None
 _LIVE = weakref.WeakSet()  # contexts / groups closed at interpreter exit (psgpu_destroy
                            # waits for an in-flight hiprtc compile: none may outlive the process)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libparsip_gpu.so")
+# A/B tooling only (tools/*_ab.sh): time another build of the library from the same tree
+LIB_PATH = os.environ.get("PSGPU_AB_LIB") or LIB_PATH
 
 
 class PsMeshInfo(ctypes.Structure):
