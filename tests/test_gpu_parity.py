@@ -272,6 +272,22 @@ def test_mpu_range_partition(gpu_poly, oracle):
     assert_mesh_matches(gpu_poly.download(), gpu_poly.stats(), om)
 
 
+def test_range_limit(gpu_poly, oracle):
+    """A range holds < 2^26 MPUs (the 8-B triangle record's slot field); a larger one is a
+    parameter error before any buffer is sized, and the context still polygonizes after."""
+    model, cs, _ = synth.make_config("C1")
+    gpu_poly.set_model(model)
+    small = np.float32(cs / 128)  # C1's box at 4096^3 cells: 585^3 MPUs
+    n = gpu.count_mpus(small, *model.bbox)
+    assert n > 1 << 26
+    for end in (None, 1 << 26):
+        with pytest.raises(gpu.PsgpuError) as e:
+            gpu_poly.polygonize(float(small), 0, end)
+        assert e.value.code == soa.RET_PARAM_ERROR
+    gm, gs, om = run_both(gpu_poly, oracle, model, cs)
+    assert_mesh_matches(gm, gs, om)
+
+
 def test_field_probe_quads(gpu_poly, oracle):
     model, cs, _ = synth.make_config("C3")
     gpu_poly.set_model(model)
