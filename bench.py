@@ -666,10 +666,10 @@ def main():
             "traffic": round(te["traffic_bytes"]) if te and "traffic_bytes" in te else None,
             "traffic_source": tr_src if te else None,
             # the bytes the launch must move (k_mpu: its records and counts out, its queue in)
-            "traffic_required": (round(8 * single.ctVertices / nparts + 12 * single.ctTriangles / nparts
+            "traffic_required": (round(8 * single.ctVertices / nparts + 8 * single.ctTriangles / nparts
                                        + 8 * single.ctMPUs / nparts + 20 * fmpus / launches)
                                  if dom == "k_mpu" else None),
-            "traffic_required_note": "k_mpu: 8 B vertex key per vertex + 12 B triangle record per triangle + "
+            "traffic_required_note": "k_mpu: 8 B vertex key per vertex + 8 B triangle record per triangle + "
                                      "8 B count per MPU written, 4 B queue entry + 16 B culling mask per "
                                      "S2-evaluated MPU read" if dom == "k_mpu" else None,
             "kernel_ms": round(dur, 4), "kernel_ms_source": "hipEvent pair around each launch on its engine's "
