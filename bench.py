@@ -79,8 +79,24 @@ def spawn_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
-    codes = [p.wait() for p in procs]
-    return max(codes, key=abs)
+    # a rank that fails (e.g. no HIP device for it) would leave the others waiting in the
+    # rendezvous forever: as torch.distributed.run does, end the remaining ranks then
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            return max(codes, key=abs)
+        if any(c not in (None, 0) for c in codes):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return max((p.returncode for p in procs), key=abs)
+        time.sleep(0.2)
 
 
 class Group:
@@ -418,6 +434,10 @@ def main():
     # (multi-rank rehearsal on a one-GPU box: the count exchange then runs over gloo)
     pinned = os.environ.get("PSGPU_BENCH_DEVICE")
     device = int(pinned) if pinned is not None else grp.local
+    ndev = gpu.device_count()
+    if device >= ndev:
+        sys.exit(f"bench.py: rank {grp.rank} needs HIP device {device} but {ndev} are visible "
+                 "(PSGPU_BENCH_DEVICE=0 runs every rank on device 0: a one-GPU rehearsal)")
     poly = gpu.Polygonizer(device)  # HIP before torch
     grp.init()
     if args.no_cull:

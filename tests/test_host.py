@@ -110,6 +110,23 @@ def test_no_device_fails_loudly():
         gpu.Polygonizer(0)
 
 
+def test_bench_ranks_end_together_without_devices():
+    """`bench.py --gpus 2` spawns its ranks; a rank without a HIP device exits with a
+    message, and the parent ends the other ranks instead of leaving them in the rendezvous."""
+    import subprocess
+    import sys
+
+    if gpu.device_count() > 0:
+        pytest.skip("a device is visible")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PSGPU_BENCH_DEVICE")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "needs HIP device" in r.stderr
+    assert r.stdout == ""
+
+
 def test_invalid_trees_rejected():
     """The walk-program builder rejects what the reference adapter rejects (-3)."""
     m, cs, _ = synth.make_config("C2")
