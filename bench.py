@@ -262,6 +262,30 @@ def latency_single(poly, cs, reps=30):
     return round(float(np.median(t)) * 1e3, 4), round(min(t) * 1e3, 4)
 
 
+def latency_single_parts(device, model, cs, jit, parts=2, reps=30):
+    """latency_single for ONE polygonization split into `parts` cost-balanced MPU ranges on
+    `parts` streams of the same device (psgpu_group over [device] * parts): the ranges'
+    kernel chains overlap each other's tails.  The parts' meshes stay separate, concatenating
+    in range order to the single-context mesh (psgpu_group_gather assembles one buffer)."""
+    g = gpu.Group([device] * parts)
+    try:
+        g.set_option(gpu.OPT_JIT, gpu.JIT_BAKED if jit == gpu.JIT_TIERED else jit)
+        g.set_model(model)
+        for _ in range(3):
+            info, _ = g.run(cs)
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            g.run(cs)
+            t.append(time.perf_counter() - t0)
+        return {"median": round(float(np.median(t)) * 1e3, 4), "best": round(min(t) * 1e3, 4), "parts": parts,
+                "vertices": info.ctVertices, "triangles": info.ctTriangles,
+                "note": f"one polygonization at a time as {parts} cost-balanced MPU ranges on {parts} streams of one "
+                        "device (psgpu_group), host-timed (enqueue + kernel chains + sync)"}
+    finally:
+        g.close()
+
+
 def blocking_contract(poly, reps=10):
     """The reference's own blocking contract, PCIe-inclusive, on C2: psgpu_polygonize_mpus =
     SimdPoly::run -> Polygonize into the caller's PolyMPUs (PS_HighPerformanceRender.cpp:373-376):
@@ -817,6 +841,7 @@ def main():
         out["latency_ms_single"] = {"median": lat[0], "best": lat[1],
                                     "note": "one engine, one polygonization at a time, host-timed "
                                             "(enqueue + kernel chain + sync): a blocking caller's latency"}
+        out["latency_ms_single_parts"] = latency_single_parts(device, model, cs, args.jit)
         out["blocking_polygonize_mpus"] = blocking_contract(poly)
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3, args.config)
