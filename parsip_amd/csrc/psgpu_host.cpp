@@ -19,6 +19,7 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/parsip_gpu.h"
@@ -993,6 +994,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hostCtr) (void)hipHostFree(c->hostCtr);
+    if (c->hostStage) (void)hipHostFree(c->hostStage);
     for (int i = 0; i <= kNumKernels; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1371,47 +1373,121 @@ int psgpu_split_costs(const uint32_t* costs, uint32_t n, uint32_t parts, uint32_
     return PSGPU_RET_SUCCESS;
 }
 
-int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt) {
+namespace {
+// The blocking export (Polygonize :360-371 into PolyMPUs, and the MPUSTATS of :372-376): one
+// batch of async copies of the compact mesh, offsets, S1 flags and (for stats) counts into the
+// context's pinned staging buffer, one wait, then the host scatter.  Pageable destinations
+// would cost a staged copy and a wait each (7 of them for a mesh plus statistics).
+int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt, PsMpuStats* stats) {
     PsMeshInfo I;
     int rc = psgpu_finish(c, &I);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     if (outCt) *outCt = c->mpuCount;
-    if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
-    if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
-    if (!mpus) return PSGPU_RET_PARAM_ERROR;
-    const size_t V = I.ctVertices, T = I.ctTriangles, N = c->mpuCount;
-    std::vector<float> pos(V * 3), nrm(V * 3), col(V * 3);
-    std::vector<uint32_t> tris(T * 3), ids;
-    std::vector<uint64_t> off(N + 1);
-    rc = psgpu_download_mesh(c, pos.data(), nrm.data(), col.data(), tris.data(), off.data());
-    if (rc != PSGPU_RET_SUCCESS) return rc;
-    rc = survivors(c, ids);
-    if (rc != PSGPU_RET_SUCCESS) return rc;
-    const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
-    for (uint32_t l = 0; l < c->mpuCount; ++l) {  // Polygonize :360-371
-        const uint32_t m = c->mpuBegin + l;
-        const uint32_t k = m % c->dims[2], j = (m / c->dims[2]) % c->dims[1], i = m / (c->dims[2] * c->dims[1]);
-        PsMPU& M = mpus[l];
-        M.bboxLo.x = c->primsHost.bboxLo.x + (float)i * side;
-        M.bboxLo.y = c->primsHost.bboxLo.y + (float)j * side;
-        M.bboxLo.z = c->primsHost.bboxLo.z + (float)k * side;
-        M.ctVertices = 0;
-        M.ctTriangles = 0;
-        M.ctFieldEvals = 0;
+    if (mpus) {
+        if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
+        if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
     }
-    for (uint32_t m : ids) mpus[m - c->mpuBegin].ctFieldEvals = 128;
-    for (size_t l = 0; l < N; ++l) {
-        PsMPU& M = mpus[l];
-        const uint32_t v0 = (uint32_t)off[l], nv = (uint32_t)off[l + 1] - v0;
-        const uint32_t t0 = (uint32_t)(off[l] >> 32), nt = (uint32_t)(off[l + 1] >> 32) - t0;
-        M.ctVertices = (uint16_t)nv;
-        M.ctTriangles = (uint16_t)nt;
-        memcpy(M.vPos, &pos[(size_t)v0 * 3], (size_t)nv * 12);
-        memcpy(M.vNorm, &nrm[(size_t)v0 * 3], (size_t)nv * 12);
-        memcpy(M.vColor, &col[(size_t)v0 * 3], (size_t)nv * 12);
-        for (uint32_t t = 0; t < nt * 3; ++t) M.triangles[t] = (uint16_t)(tris[(size_t)t0 * 3 + t] - v0);
+    if (!mpus && !stats) return PSGPU_RET_PARAM_ERROR;
+    const size_t V = mpus ? I.ctVertices : 0, T = mpus ? I.ctTriangles : 0, N = c->mpuCount;
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t oOffs = 0, oPos = up(oOffs + (N + 1) * 8), oNrm = up(oPos + V * 12), oCol = up(oNrm + V * 12),
+                 oTris = up(oCol + V * 12), oPass = up(oTris + T * 12), oCnt = up(oPass + N),
+                 total = up(oCnt + (stats ? N * 8 : 0));
+    if (total > c->hostStageCap) {
+        if (c->hostStage) (void)hipHostFree(c->hostStage);
+        c->hostStage = nullptr;
+        c->hostStageCap = 0;
+        const size_t cap = total + total / 4;
+        PSGPU_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c->hostStage), cap, hipHostMallocDefault));
+        c->hostStageCap = cap;
+    }
+    unsigned char* h = c->hostStage;
+    hipStream_t s = c->stream;
+    if (N) {
+        if (mpus) PSGPU_CHECK(hipMemcpyAsync(h + oOffs, c->offs, (N + 1) * 8, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + oPass, c->passed, N, hipMemcpyDeviceToHost, s));
+        if (stats) PSGPU_CHECK(hipMemcpyAsync(h + oCnt, c->counts, N * 8, hipMemcpyDeviceToHost, s));
+    }
+    if (V) {
+        PSGPU_CHECK(hipMemcpyAsync(h + oPos, c->pos, V * 12, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + oNrm, c->nrm, V * 12, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + oCol, c->col, V * 12, hipMemcpyDeviceToHost, s));
+    }
+    if (T) PSGPU_CHECK(hipMemcpyAsync(h + oTris, c->tris, T * 12, hipMemcpyDeviceToHost, s));
+    PSGPU_CHECK(hipStreamSynchronize(s));
+    const uint64_t* off = reinterpret_cast<const uint64_t*>(h + oOffs);
+    const float* pos = reinterpret_cast<const float*>(h + oPos);
+    const float* nrm = reinterpret_cast<const float*>(h + oNrm);
+    const float* col = reinterpret_cast<const float*>(h + oCol);
+    const uint32_t* tris = reinterpret_cast<const uint32_t*>(h + oTris);
+    const uint8_t* passed = h + oPass;
+    if (mpus) {
+        const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
+        // the scatter is bound by the write-allocates of the sparse PolyMPUs layout (21.5 KB per
+        // MPU): several host threads, as the reference's TBB bodies fill it
+        auto scatter = [&](uint32_t lb, uint32_t le) {
+        for (uint32_t l = lb; l < le; ++l) {  // Polygonize :360-371
+            const uint32_t m = c->mpuBegin + l;
+            const uint32_t k = m % c->dims[2], j = (m / c->dims[2]) % c->dims[1], i = m / (c->dims[2] * c->dims[1]);
+            PsMPU& M = mpus[l];
+            M.bboxLo.x = c->primsHost.bboxLo.x + (float)i * side;
+            M.bboxLo.y = c->primsHost.bboxLo.y + (float)j * side;
+            M.bboxLo.z = c->primsHost.bboxLo.z + (float)k * side;
+            M.ctFieldEvals = passed[l] ? 128 : 0;
+            const uint32_t v0 = (uint32_t)off[l], nv = (uint32_t)off[l + 1] - v0;
+            const uint32_t t0 = (uint32_t)(off[l] >> 32), nt = (uint32_t)(off[l + 1] >> 32) - t0;
+            M.ctVertices = (uint16_t)nv;
+            M.ctTriangles = (uint16_t)nt;
+            memcpy(M.vPos, pos + (size_t)v0 * 3, (size_t)nv * 12);
+            memcpy(M.vNorm, nrm + (size_t)v0 * 3, (size_t)nv * 12);
+            memcpy(M.vColor, col + (size_t)v0 * 3, (size_t)nv * 12);
+            for (uint32_t t = 0; t < nt * 3; ++t) M.triangles[t] = (uint16_t)(tris[(size_t)t0 * 3 + t] - v0);
+        }
+        };
+        const size_t bytes = (V + T) * 12;  // ~1 thread per 256 KB of mesh, at most 8
+        const uint32_t nth = (uint32_t)std::min<size_t>({8, std::max(1u, std::thread::hardware_concurrency()),
+                                                        1 + bytes / (256 << 10)});
+        if (nth <= 1) {
+            scatter(0, (uint32_t)N);
+        } else {
+            // chunks of 128 MPUs dealt round robin (the surface lies in a few slabs of the range)
+            auto strided = [&](uint32_t k) {
+                for (uint32_t b = k * 128u; b < N; b += nth * 128u) scatter(b, std::min<uint32_t>((uint32_t)N, b + 128u));
+            };
+            std::vector<std::thread> th;
+            for (uint32_t k = 1; k < nth; ++k) th.emplace_back(strided, k);
+            strided(0);
+            for (std::thread& t : th) t.join();
+        }
+    }
+    if (stats) {
+        const uint64_t* cnt = reinterpret_cast<const uint64_t*>(h + oCnt);
+        memset(stats, 0, sizeof(PsMpuStats) * N);
+        for (uint32_t l = 0; l < N; ++l) {
+            PsMpuStats& st = stats[l];
+            if (passed[l]) {
+                st.passedPrecheck = 1;
+                st.ctFieldEvals = 128;
+            }
+            st.ctVertices = (uint32_t)(cnt[l] & 0xffffffffu);
+            st.ctTriangles = (uint32_t)(cnt[l] >> 32);
+        }
     }
     return PSGPU_RET_SUCCESS;
+}
+}  // namespace
+
+int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt) {
+    if (!mpus) {  // the count (and overflow) check alone
+        PsMeshInfo I;
+        int rc = psgpu_finish(c, &I);
+        if (rc != PSGPU_RET_SUCCESS) return rc;
+        if (outCt) *outCt = c->mpuCount;
+        if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
+        if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
+        return PSGPU_RET_PARAM_ERROR;
+    }
+    return export_blocking(c, mpus, capacity, outCt, nullptr);
 }
 
 int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats,
@@ -1423,10 +1499,11 @@ int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* pr
     if (rc != PSGPU_RET_SUCCESS) return rc;
     rc = psgpu_polygonize(c, cellsize, 0, 0xffffffffu, nullptr);
     if (rc != PSGPU_RET_SUCCESS) return rc;
-    rc = psgpu_export_polympus(c, mpus, capacity, outCt);
-    if (rc != PSGPU_RET_SUCCESS) return rc;
-    if (stats) rc = psgpu_download_stats(c, stats);
-    return rc;
+    if (!mpus) {  // the reference's own errors first (count, overflow), then the null
+        rc = psgpu_export_polympus(c, nullptr, capacity, outCt);
+        return rc;
+    }
+    return export_blocking(c, mpus, capacity, outCt, stats);
 }
 
 // Field probe (FieldComputer::fieldValue / fieldValueAndColor on arbitrary points).

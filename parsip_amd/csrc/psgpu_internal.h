@@ -108,6 +108,8 @@ struct psgpu_ctx {
     uint32_t spanCap = 0, spanNext = 0;
     DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
     DevCounters* hostCtrDev = nullptr;  // its device address
+    unsigned char* hostStage = nullptr;  // pinned staging for the blocking PolyMPUs export
+    size_t hostStageCap = 0;
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
     uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
     hipEvent_t ev[kNumKernels + 1] = {};
