@@ -1455,7 +1455,13 @@ int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outC
                 for (uint32_t b = k * 128u; b < N; b += nth * 128u) scatter(b, std::min<uint32_t>((uint32_t)N, b + 128u));
             };
             std::vector<std::thread> th;
-            for (uint32_t k = 1; k < nth; ++k) th.emplace_back(strided, k);
+            for (uint32_t k = 1; k < nth; ++k) {
+                try {
+                    th.emplace_back(strided, k);
+                } catch (...) {  // no thread to be had: this caller does the chunks itself
+                    strided(k);
+                }
+            }
             strided(0);
             for (std::thread& t : th) t.join();
         }
