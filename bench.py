@@ -147,13 +147,18 @@ class Group:
         return [o.tolist() for o in out]
 
 
-def committed_profile(kind: str):
-    """Newest committed rocprofv3 summary of `kind` (profiles/rNN*_<kind>.json)."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{kind}.json")), reverse=True):
+def committed_profile(kind: str, jit: int):
+    """Newest committed rocprofv3 summary of `kind` (profiles/rNN_<kind>.json) profiled on the
+    kernels of OPT_JIT mode `jit` (the file's "jit"; files from before r04 carry none and were
+    profiled with --jit 2)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{kind}.json")), reverse=True):
         try:
             with open(path) as f:
-                return json.load(f)["kernels"], os.path.relpath(path, ROOT)
-        except (OSError, ValueError, KeyError):
+                d = json.load(f)
+            if int(d.get("jit", 2)) != jit:
+                continue
+            return d["kernels"], os.path.relpath(path, ROOT)
+        except (OSError, ValueError, KeyError, TypeError):
             continue
     return None, None
 
@@ -570,8 +575,11 @@ def main():
         grp.barrier()
         ms1 = grp.max(time.perf_counter() - t0) / args.steps * 1e3
         tiers1 = [e.jit_tier() for e in engines]
+        # tier up now: every engine has run the unchanged model at least once, so with a
+        # threshold of 1 its next run starts the baked compile (a short --steps never reaches
+        # the library's default of TIER_RUNS runs per engine); wait for the swap
         for e in engines:
-            e.set_option(gpu.OPT_TIER_RUNS, TIER_RUNS)
+            e.set_option(gpu.OPT_TIER_RUNS, 1)
         tt = time.perf_counter()
         for k in range(neng):
             engines[k].polygonize()
@@ -580,15 +588,22 @@ def main():
             e.jit_wait()
         t_tier = time.perf_counter() - tt
         tiers2 = [e.jit_tier() for e in engines]
+        timed_jit = gpu.JIT_BAKED if all(t == 2 for t in tiers2) else gpu.JIT_STRUCTURE
+        # every rank must time the same tier (a rank whose baked compile failed keeps the
+        # structure kernels): the headline is labelled by the lowest tier over the ranks
+        if grp.max(0.0 if timed_jit == gpu.JIT_BAKED else 1.0) > 0.0:
+            timed_jit = gpu.JIT_STRUCTURE
         tier = {"structure_kernels": {"ms_per_step": round(ms1, 4),
                                       "value": round(N ** 3 * (grp.world if scaling == "weak" else 1) / (ms1 * 1e-3) / 1e6, 2),
                                       "tiers": tiers1},
-                "tier_up_runs": TIER_RUNS, "baked_ready_s": round(t_tier, 3), "tiers": tiers2,
+                "tier_up_after_runs": 1, "baked_ready_s": round(t_tier, 3),
                 "note": "the same K steps on the structure-specialised kernels (parameters read from the model in "
-                        "HBM) before the tier-up; value is measured on the baked kernels (parameters compiled "
-                        "in as literals) that replace them once the model has stayed unchanged for "
-                        f"{TIER_RUNS} runs; baked_ready_s = the tier-up run to the kernels' swap (hiprtc compile "
-                        "or on-disk code-object cache)"}
+                        "HBM) before the tier-up; then every engine tiers up (OPT_TIER_RUNS 1: the library's "
+                        f"default waits for {TIER_RUNS} unchanged runs) and the headline is timed on the tier in "
+                        "config.tiers (2 = baked: parameters compiled in as literals); baked_ready_s = the tier-up "
+                        "run to the kernels' swap (hiprtc compile or on-disk code-object cache)"}
+    else:
+        timed_jit = args.jit
     for k in range(max(args.warmup, neng)):
         engines[k % neng].polygonize()
     for e in engines:
@@ -697,13 +712,16 @@ def main():
     # device-clock span of the replay beside it
     dur = ev_ms.get(dom) or kt[dom]
     achieved = alg_ops / (dur * 1e-3) / 1e12
-    # the committed PMC / traffic passes profile the baked kernels (tools/gpu_round.sh: --jit 2, the
-    # kernels tier 2 of the default --jit 3 runs)
-    prof_ok = args.config == "C3" and grp.world == 1 and (nparts, neng) == (1, ENGINES_DEFAULT) and args.jit in (2, 3)
-    pmc, pmc_src = committed_profile("pmc")
-    pe = profile_entry(pmc, dom, args.jit) if prof_ok else None
-    tr, tr_src = committed_profile("traffic")
-    te = profile_entry(tr, dom, args.jit) if prof_ok else None
+    # the committed PMC / traffic passes of the tier that was timed (tools/gpu_round.sh profiles
+    # the bench command twice: --jit 2, the baked kernels -> rNN_pmc.json / rNN_traffic.json;
+    # --jit 1, the structure kernels -> rNN_pmc_structure.json / rNN_traffic_structure.json;
+    # each file records the jit mode it ran)
+    prof_ok = args.config == "C3" and grp.world == 1 and (nparts, neng) == (1, ENGINES_DEFAULT) and timed_jit in (1, 2)
+    suffix = "" if timed_jit == gpu.JIT_BAKED else "_structure"
+    pmc, pmc_src = committed_profile("pmc" + suffix, timed_jit)
+    pe = profile_entry(pmc, dom, timed_jit) if prof_ok else None
+    tr, tr_src = committed_profile("traffic" + suffix, timed_jit)
+    te = profile_entry(tr, dom, timed_jit) if prof_ok else None
     lk = {"bound": "valu", "pipe": "fp32 VALU (no MFMA: scalar field evaluation; SURVEY.md §8(d))",
             "kernel": dom, "achieved": round(achieved, 3), "peak": NOFMA_PEAK_TOPS, "unit": "T op/s",
             "frac": round(achieved / NOFMA_PEAK_TOPS, 4),
@@ -762,7 +780,7 @@ def main():
     step = None
     if pmc and prof_ok:
         ks = {k: v for k, v in pmc.items() if "SQ_INSTS_VALU" in v and "probe" not in k}
-        first = profile_entry(pmc, "k_precheck", args.jit)
+        first = profile_entry(pmc, "k_precheck", timed_jit)
         steps_prof = (first or {}).get("launches")
         if ks and steps_prof:
             instr = sum(v["SQ_INSTS_VALU"] * v.get("launches", steps_prof) for v in ks.values()) / steps_prof
@@ -770,7 +788,7 @@ def main():
             issue = instr * 2 / (sec * 2.4e9 * 1024)
             lane_tops = instr * 64 / sec / 1e12
             tr_step = None
-            tfirst = profile_entry(tr, "k_precheck", args.jit) if tr else None
+            tfirst = profile_entry(tr, "k_precheck", timed_jit) if tr else None
             if tfirst and tfirst.get("calls"):  # launches per step from the kernel-trace call counts
                 tr_step = sum(v.get("traffic_bytes", 0.0) * v.get("calls", tfirst["calls"]) / tfirst["calls"]
                               for k, v in tr.items() if "probe" not in k)
@@ -792,6 +810,15 @@ def main():
     roof = step if step else dict(lk)
     roof["per_launch"] = lk
 
+    # what the timed steps ran, per engine: 0 interpreter, 1 structure kernels, 2 baked kernels
+    tiers_timed = [e.jit_tier() for e in engines]
+    if args.jit and not jit_on:
+        kernels_label = "interpreter (jit unavailable)"
+    elif args.jit == gpu.JIT_TIERED:
+        kernels_label = ("jit-tiered: baked tier" if timed_jit == gpu.JIT_BAKED
+                         else "jit-tiered: structure tier (the baked kernels were not ready)")
+    else:
+        kernels_label = ["interpreter", "jit-structure", "jit-baked"][args.jit]
     out = {
         "metric": METRIC if args.config == "C3" else METRIC_OTHER.format(
             n=N, p=model.ct_prims, config=args.config, g=grp.world),
@@ -818,8 +845,7 @@ def main():
                            "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
                    "exchange": exchange, "culling": not args.no_cull, "tree_split": args.tree_split,
-                   "kernels": ["interpreter", "jit-structure", "jit-baked", "jit-tiered"][args.jit] if jit_on or args.jit == 0
-                   else "interpreter (jit unavailable)", "set_model_s": round(t_model, 4),
+                   "kernels": kernels_label, "tiers": tiers_timed, "set_model_s": round(t_model, 4),
                    "jit_ready_s": round(t_jit, 3)},
         "roofline": roof,
         "kernel_ms_per_launch": {k: round(v, 4) for k, v in kt.items()},

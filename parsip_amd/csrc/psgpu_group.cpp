@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -87,6 +88,17 @@ bool same_lattice(const psgpu_group* g, float cs) {
            !memcmp(&g->planHi, &P.bboxHi, sizeof(PsVec3f));
 }
 
+// MPUs per planning run: below the per-run limit (PSGPU_PLAN_CHUNK_MPUS lowers it, so tests
+// exercise the chunked plan on small lattices)
+uint32_t plan_chunk_mpus() {
+    uint32_t chunk = kMaxRangeMpus - 1u;
+    if (const char* v = getenv("PSGPU_PLAN_CHUNK_MPUS")) {
+        const long x = strtol(v, nullptr, 10);
+        if (x > 0 && (uint64_t)x < chunk) chunk = (uint32_t)x;
+    }
+    return chunk;
+}
+
 void even_split(psgpu_group* g, uint32_t total) {
     const uint32_t n = (uint32_t)g->parts.size();
     g->bounds.assign(n + 1, 0);
@@ -94,19 +106,24 @@ void even_split(psgpu_group* g, uint32_t total) {
 }
 
 // Cost split of the lattice from a planning run of the whole grid on part 0 (one
-// polygonization; results are exact, so every caller that plans the same model and
-// lattice gets the same split).
+// polygonization per chunk of fewer than kMaxRangeMpus MPUs, the most one run takes;
+// results are exact, so every caller that plans the same model and lattice gets the same
+// split).
 int plan(psgpu_group* g, float cs, uint32_t total) {
     const uint32_t n = (uint32_t)g->parts.size();
     g->bounds.assign(n + 1, 0);
     g->bounds[n] = total;
     if (n > 1 && total > 0) {
-        int rc = psgpu_polygonize(g->parts[0], cs, 0, total, nullptr);
-        if (rc != PSGPU_RET_SUCCESS) return rc;
         std::vector<uint32_t> costs(total);
-        rc = psgpu_mpu_costs(g->parts[0], costs.data());
-        if (rc != PSGPU_RET_SUCCESS) return rc;
-        rc = psgpu_split_costs(costs.data(), total, n, 0, g->bounds.data());
+        for (uint32_t b = 0; b < total;) {
+            const uint32_t e = (uint32_t)std::min<uint64_t>(total, (uint64_t)b + plan_chunk_mpus());
+            int rc = psgpu_polygonize(g->parts[0], cs, b, e, nullptr);
+            if (rc != PSGPU_RET_SUCCESS) return rc;
+            rc = psgpu_mpu_costs(g->parts[0], costs.data() + b);
+            if (rc != PSGPU_RET_SUCCESS) return rc;
+            b = e;
+        }
+        const int rc = psgpu_split_costs(costs.data(), total, n, 0, g->bounds.data());
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
     const PsSoaBlobPrims& P = g->parts[0]->primsHost;
@@ -488,7 +505,7 @@ int psgpu_comm_create(psgpu_ctx* ctx, const uint8_t id[PSGPU_COMM_ID_BYTES], int
         (hipMalloc(&m->gathered, (size_t)nranks * 8 * sizeof(uint32_t)) != hipSuccess ||
          hipHostMalloc(&m->hostGathered, (size_t)nranks * 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
          hipMalloc(&m->flag, sizeof(uint32_t)) != hipSuccess ||
-         hipHostMalloc(&m->hostFlag, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess))
+         hipHostMalloc(&m->hostFlag, 9 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess))
         rc = PSGPU_RET_DEVICE_ERROR;
     if (rc != PSGPU_RET_SUCCESS) {
         psgpu_comm_destroy(m);
@@ -568,27 +585,49 @@ int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
 // exchanged; whether any rank did so is itself agreed collectively (an all-reduce MAX of a
 // flag, on every rank), and then EVERY rank exchanges again -- a collective entered by only
 // the ranks that re-ran would block them forever and leave the others with stale counts.
+// A rank whose finish fails still enters the all-reduce, with flag 2: then every rank
+// returns an error (its own, or PSGPU_RET_DEVICE_ERROR for another rank's failure) and
+// none waits for a collective the failed rank will not enter.
 int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut) {
     if (!m || !m->pending || !m->ctx) return PSGPU_RET_PARAM_ERROR;
     psgpu_ctx* c = m->ctx;
     PsMeshInfo mine;
-    int rc = m->group ? psgpu_group_finish(m->group, &mine, nullptr) : psgpu_finish(c, &mine);
-    if (rc != PSGPU_RET_SUCCESS) return rc;
-    rc = set_device(c);
-    if (rc != PSGPU_RET_SUCCESS) return rc;
+    int local = m->group ? psgpu_group_finish(m->group, &mine, nullptr) : psgpu_finish(c, &mine);
+    m->pending = false;
+    if (hipSetDevice(m->device) != hipSuccess) return local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR;
     hipStream_t s = c->runStream ? c->runStream : c->stream;
-    // the gathered totals of the last exchange come to the host only here (not per step:
-    // one HIP call less on the host's enqueue path, which bounds small rank shares)
     const size_t gb = (size_t)m->nranks * 8 * sizeof(uint32_t);
-    PSGPU_CHECK(hipMemcpyAsync(m->hostGathered, m->gathered, gb, hipMemcpyDeviceToHost, s));
-    PSGPU_CHECK(hipStreamSynchronize(s));
-    const uint32_t* mineG = m->hostGathered + 8 * m->rank;
-    *m->hostFlag = (mineG[0] != mine.ctMPUs || mineG[1] != mine.ctVertices || mineG[2] != mine.ctTriangles) ? 1u : 0u;
-    PSGPU_CHECK(hipMemcpyAsync(m->flag, m->hostFlag, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    rc = nccl_fail(ncclAllReduce(m->flag, m->flag, 1, ncclUint32, ncclMax, m->comm, s), "ncclAllReduce");
-    if (rc != PSGPU_RET_SUCCESS) return rc;
+    uint32_t flag = 2u;
+    if (local == PSGPU_RET_SUCCESS) {
+        // this rank's totals as exchanged vs the totals of its final run (all 8 words: counts,
+        // the first overflowing MPU, the error word), both to the host in one wait; the
+        // gathered words come to the host only here (not per step: one HIP call less on the
+        // host's enqueue path, which bounds small rank shares)
+        const uint32_t* finalWords = c->totals;
+        if (m->group && m->group->sumTotals) {  // the parts' final totals, summed as exchange_group does
+            TotalsParts tp{};
+            tp.n = (int)m->group->parts.size();
+            for (size_t k = 0; k < m->group->parts.size(); ++k) tp.p[k] = m->group->parts[k]->totals;
+            if (launch_sum_totals(tp, m->group->sumTotals, s) != hipSuccess) local = PSGPU_RET_DEVICE_ERROR;
+            finalWords = m->group->sumTotals;
+        }
+        if (local == PSGPU_RET_SUCCESS &&
+            (hipMemcpyAsync(m->hostGathered, m->gathered, gb, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipMemcpyAsync(m->hostFlag + 1, finalWords, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess))
+            local = PSGPU_RET_DEVICE_ERROR;
+        if (local == PSGPU_RET_SUCCESS)
+            flag = memcmp(m->hostGathered + 8 * m->rank, m->hostFlag + 1, 8 * sizeof(uint32_t)) != 0 ? 1u : 0u;
+    }
+    *m->hostFlag = flag;
+    if (hipMemcpyAsync(m->flag, m->hostFlag, sizeof(uint32_t), hipMemcpyHostToDevice, s) != hipSuccess)
+        return local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR;
+    int rc = nccl_fail(ncclAllReduce(m->flag, m->flag, 1, ncclUint32, ncclMax, m->comm, s), "ncclAllReduce");
+    if (rc != PSGPU_RET_SUCCESS) return local != PSGPU_RET_SUCCESS ? local : rc;
     PSGPU_CHECK(hipMemcpyAsync(m->hostFlag, m->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     PSGPU_CHECK(hipStreamSynchronize(s));
+    if (local != PSGPU_RET_SUCCESS) return local;
+    if (*m->hostFlag >= 2u) return PSGPU_RET_DEVICE_ERROR;  // another rank's finish failed
     m->reexchanged = *m->hostFlag != 0u;
     if (m->reexchanged) {  // some rank's totals changed after the exchange: all ranks exchange again
         rc = m->group ? psgpu_comm_exchange_group(m, m->group) : psgpu_comm_exchange(m, c);

@@ -1116,13 +1116,17 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     if (rc != PSGPU_RET_SUCCESS) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->pending && c->runStream != s) (void)hipStreamSynchronize(c->runStream);
-    c->cs = cellsize;
-    lattice_dims(cellsize, c->primsHost.bboxLo, c->primsHost.bboxHi, c->dims);
-    const uint64_t total = (uint64_t)c->dims[0] * c->dims[1] * c->dims[2];
+    // validate into locals first: a rejected call leaves the lattice of a pending run (its
+    // finish / export read c->cs and c->dims) untouched
+    uint32_t dims[3];
+    lattice_dims(cellsize, c->primsHost.bboxLo, c->primsHost.bboxHi, dims);
+    const uint64_t total = (uint64_t)dims[0] * dims[1] * dims[2];
     if (total > 0xffffffffull) return PSGPU_RET_PARAM_ERROR;
     const uint32_t end = (uint32_t)std::min<uint64_t>(mpuEnd, total);
     const uint32_t begin = std::min(mpuBegin, end);
     if (end - begin >= kMaxRangeMpus) return PSGPU_RET_PARAM_ERROR;  // TriRec's 20-bit slot field
+    c->cs = cellsize;
+    memcpy(c->dims, dims, sizeof(dims));
     if (begin != c->mpuBegin || end - begin != c->mpuCount || cellsize != c->lastCs) {
         // another range or lattice: the last run's survivor count says nothing about this
         // one -- size k_mpu for the whole range (no re-run) until a run of it finishes.  A new
@@ -1203,6 +1207,10 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         const DevCounters& h = *c->hostCtr;
         if (c->mpuCount && h.error) {
             fprintf(stderr, "psgpu: device protocol error 0x%x\n", h.error);
+            return PSGPU_RET_DEVICE_ERROR;
+        }
+        if (c->debug & (1 << 21)) {  // test hook: this finish fails as a protocol error would (one run)
+            c->debug &= ~(1 << 21);
             return PSGPU_RET_DEVICE_ERROR;
         }
         uint32_t V = 0, T = 0, S = 0, P = 0, Q = 0;

@@ -101,6 +101,25 @@ def test_group_c2_policies_match_oracle(group8, oracle, policy):
     assert_mesh_matches(mesh, st, om)
 
 
+def test_group_plan_in_chunks_equals_one_run(gpu_poly, monkeypatch):
+    """The planning run goes in chunks of fewer MPUs than one run takes (2^26; lowered here
+    to 1,000 so C2's 6,859 MPUs plan in 7 runs): the split equals the one-run plan's."""
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+    gpu_poly.run(cs)
+    want = [int(x) for x in gpu.split_costs(gpu_poly.mpu_costs(), 3)]
+    monkeypatch.setenv("PSGPU_PLAN_CHUNK_MPUS", "1000")
+    g = gpu.Group([0] * 3)
+    try:
+        g.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+        g.set_model(model)
+        info, _ = g.run(cs)
+        assert [int(x) for x in g.split()] == want
+        assert info.ctVertices == gpu_poly.finish().ctVertices
+    finally:
+        g.close()
+
+
 def test_group_fixed_split_with_empty_parts(group8, oracle):
     model, cs, _ = synth.make_config("C2")
     n = gpu.count_mpus(cs, *model.bbox)
@@ -174,6 +193,32 @@ def test_rccl_exchange_after_rerun_single_rank(gpu_poly):
         comm.close()
 
 
+def test_rccl_result_after_failed_finish_single_rank(gpu_poly):
+    """A rank whose finish fails (test hook: debug bit 21) still enters the collective flag
+    all-reduce and returns the failure; the communicator stays usable for the next step."""
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+    comm = gpu.Comm(gpu_poly, gpu.comm_unique_id(), 1, 0)
+    try:
+        gpu_poly.polygonize(cs)
+        comm.exchange()
+        ref, _ = comm.result()
+        gpu_poly.set_option(gpu.OPT_DEBUG, 1 << 21)
+        gpu_poly.polygonize(cs)
+        comm.exchange()
+        with pytest.raises(gpu.PsgpuError) as e:
+            comm.result()
+        assert e.value.code == -6
+        gpu_poly.polygonize(cs)
+        comm.exchange()
+        total, _ = comm.result()
+        assert not comm.reexchanged()
+        assert (total.ctMPUs, total.ctVertices, total.ctTriangles) == (ref.ctMPUs, ref.ctVertices, ref.ctTriangles)
+    finally:
+        gpu_poly.set_option(gpu.OPT_DEBUG, 0)
+        comm.close()
+
+
 _TWO_RANK = r"""
 import os, sys
 sys.path.insert(0, os.environ["PSGPU_ROOT"])
@@ -197,6 +242,19 @@ comm.exchange()
 total, parts = comm.result()
 assert comm.reexchanged(), rank
 assert (total.ctMPUs, total.ctVertices, total.ctTriangles) == (full.ctMPUs, full.ctVertices, full.ctTriangles)
+if rank == 0:  # only this rank's finish fails: both ranks return an error, neither blocks
+    poly.set_option(gpu.OPT_DEBUG, 1 << 21)
+poly.polygonize(cs, int(b[rank]), int(b[rank + 1]))
+comm.exchange()
+try:
+    comm.result()
+    raise AssertionError(f"rank {rank}: result() succeeded after rank 0's finish failed")
+except gpu.PsgpuError as e:
+    assert e.code == -6, (rank, e.code)
+poly.polygonize(cs, int(b[rank]), int(b[rank + 1]))  # and the next step works on both
+comm.exchange()
+total, parts = comm.result()
+assert (total.ctMPUs, total.ctVertices, total.ctTriangles) == (full.ctMPUs, full.ctVertices, full.ctTriangles)
 comm.close()
 poly.close()
 dist.destroy_process_group()
@@ -206,7 +264,8 @@ print("ok", rank)
 
 def test_rccl_two_ranks_one_rerun(tmp_path):
     """Two ranks over RCCL where only rank 1's finish re-runs: the re-exchange is agreed
-    collectively, so neither rank blocks and both get the re-run's totals (needs 2 GPUs)."""
+    collectively, so neither rank blocks and both get the re-run's totals; then only rank
+    0's finish fails and both ranks return the error instead of blocking (needs 2 GPUs)."""
     if gpu.device_count() < 2:
         pytest.skip("needs two GPUs (RCCL ranks on distinct devices)")
     import socket

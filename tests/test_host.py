@@ -4,6 +4,8 @@ the run-time specialised kernels compile.  No compute call needs a device here."
 import glob
 import os
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -143,6 +145,33 @@ def test_jit_compiles_c3(mode):
     """hiprtc specialisation of the C3 tree compiles for gfx950 without a device."""
     m, _, _ = synth.make_config("C3")
     assert gpu.jit_compile(m, mode) > 10000
+
+
+_JIT_TREES = r"""
+import os, sys
+sys.path.insert(0, os.environ["PSGPU_ROOT"])
+from parsip_amd import gpu, synth
+from parsip_amd.soa import NodeType
+ops = [NodeType.BLEND, NodeType.UNION, NodeType.INTERSECT, NodeType.DIF, NodeType.SMOOTHDIF,
+       NodeType.RICCIBLEND, NodeType.WARPTWIST, NodeType.WARPTAPER, NodeType.WARPBEND, NodeType.WARPSHEAR]
+types = [NodeType.POINT, NodeType.LINE, NodeType.CYLINDER, NodeType.CUBE, NodeType.DISC, NodeType.RING,
+         NodeType.TRIANGLE]
+for seed, n in ((1, 6), (2, 17), (3, 40)):
+    m = synth.random_model(seed, n, types=types, op_types=ops, matrices=seed % 2 == 1)
+    assert gpu.jit_compile(m, 2) > 1000, seed
+print("ok")
+"""
+
+
+def test_baked_tier_compiles_random_trees_in_process_safe_flags(tmp_path):
+    """The baked tier compiles on a host thread of the caller's process, so its flags must
+    never crash hiprtc: random trees with every primitive and operator type compile with the
+    default flags (LLVM's default scheduler; r03's experimental strategies crashed hiprtc),
+    in a child process so a crash fails this test instead of the runner."""
+    env = dict(os.environ, PSGPU_ROOT=ROOT, PSGPU_JIT_CACHE=str(tmp_path / "jitcache"))
+    env.pop("PSGPU_JIT_BAKED_FLAGS", None)
+    r = subprocess.run([sys.executable, "-c", _JIT_TREES], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stderr[-2000:])
 
 
 def test_cpp_shim_compiles_and_runs(tmp_path):

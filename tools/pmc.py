@@ -1,7 +1,8 @@
 """Per-kernel PMC summary (per launch, averaged) from the passes of tools/pmc.sh, with
 derived issue figures: VALU issue utilisation at 2 cycles per wave64 VALU instruction
 (CDNA4 SIMD-32, MI355X_MICROARCH.md "Wave scheduling"), waves per SIMD, stall shares.
-Usage: python tools/pmc.py gpurun_out/<tag>  -> JSON on stdout."""
+Usage: python tools/pmc.py gpurun_out/<tag> [JIT]  -> JSON on stdout (JIT: the bench's --jit of the
+profiled command, recorded as "jit")."""
 import collections
 import csv
 import glob
@@ -21,6 +22,8 @@ for p in glob.glob(os.path.join(d, "p*", "**", "*kernel_trace.csv"), recursive=T
 out = {"note": "per launch; mean_waves_per_simd = SQ_WAVE_CYCLES x 4 / (us x 2400 x 1024); valu_issue = SQ_INSTS_VALU x 2 cyc / (us x 2400 x 1024 SIMDs); SQ_*_CYCLES and "
                "SQ_WAIT_* count quad-cycles (MI355X_MICROARCH.md); profiled clocks run lower than un-profiled",
        "kernels": {}}
+if len(sys.argv) > 2:
+    out["jit"] = int(sys.argv[2])
 for k, c in acc.items():
     if "rocclr" in k or "__amd" in k:
         continue
