@@ -432,10 +432,9 @@ def main():
                     help="skip the single-polygonization latency and the blocking C2 Polygonize timing")
     ap.add_argument("--no-cull", action="store_true", help="disable exact primitive culling")
     ap.add_argument("--jit", type=int, default=None, choices=[0, 1, 2, 3],
-                    help="0 interpreter, 1 kernels specialised per tree structure, 2 + parameters baked in, "
-                         "3 tiered: structure kernels, then baked ones once the model has stayed unchanged for "
-                         f"{TIER_RUNS} runs (default 3 for the static configs; 1 for C5, whose parameters "
-                         "change every frame)")
+                    help="0 interpreter, 1 kernels specialised per tree structure (default), 2 + parameters baked "
+                         "in, 3 tiered: the structure kernels' pass, then the baked ones (tier-up forced before the "
+                         "headline, which is timed and labelled on the tier reached)")
     ap.add_argument("--tree-split", type=int, default=None, choices=[0, 1, 2],
                     help="OPT_TREE_SPLIT: 1 walk the root's two subtrees in two waves per brick / MPU, 2 only on "
                          "launches that queue few MPUs (default: 2 for strong scaling over N > 1 ranks, whose "
@@ -455,7 +454,11 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={grp.world}: launch one process per GPU")
     scaling = args.scaling or ("strong" if grp.world > 1 else "weak")
     if args.jit is None:
-        args.jit = gpu.JIT_STRUCTURE if args.config == "C5" else gpu.JIT_TIERED
+        # the structure-specialised kernels: measured faster than the baked ones in the
+        # 4-engine throughput regime since r04 (C3, 200 steps, 3 interleaved runs on one box:
+        # 0.0563 vs 0.0590 ms/step, profiles/r04_tier_ab.txt); C5 changes its parameters every
+        # frame, so it never leaves this tier anyway
+        args.jit = gpu.JIT_STRUCTURE
     if args.tree_split is None:
         args.tree_split = 2 if scaling == "strong" and grp.world > 1 else 0
 

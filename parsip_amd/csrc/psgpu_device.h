@@ -759,7 +759,12 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const uint32_t mg = (mi * p.dims[1] + mj) * p.dims[2] + mk;
     const bool valid = W < nBricks && mi < p.dims[0] && mj < p.dims[1] && mk < p.dims[2] && mg >= p.mpuBegin &&
                        mg - p.mpuBegin < p.mpuCount;
-    const uint32_t m = valid ? mg : p.mpuBegin;
+    // A lane without an MPU of the range (a brick over the lattice's high faces or a range
+    // end) takes the origin of the nearest lattice MPU, so the wave's culling box stays the
+    // brick's: with MPU 0's origin there, the box of each of C3's 1,027 face bricks spans
+    // the domain, every primitive stays live and those waves walk 3-5x longer (r03 timeline).
+    const uint32_t ci = min(mi, p.dims[0] - 1u), cj = min(mj, p.dims[1] - 1u), ck = min(mk, p.dims[2] - 1u);
+    const uint32_t m = valid ? mg : (ci * p.dims[1] + cj) * p.dims[2] + ck;
     float o[3];
     mpu_origin(p, m, o);
     const int c = lane & 7;
