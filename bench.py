@@ -291,28 +291,34 @@ def latency_single_parts(device, model, cs, jit, parts=2, reps=30):
         g.close()
 
 
-def blocking_contract(poly, reps=10):
-    """The reference's own blocking contract, PCIe-inclusive, on C2: psgpu_polygonize_mpus =
-    SimdPoly::run -> Polygonize into the caller's PolyMPUs (PS_HighPerformanceRender.cpp:373-376):
-    model upload, polygonization, mesh download and the scatter into the reference-capacity
-    (24,000 x 21.5 KB) PolyMPUs layout.  Median over `reps` calls after 2 warm-ups."""
+def blocking_contract(poly, config="C2", reps=10):
+    """The reference's own blocking contract, PCIe-inclusive: Polygonize into the caller's
+    PolyMPUs (PS_Polygonizer.h:386-391 as SimdPoly::run calls it, PS_HighPerformanceRender.cpp:
+    373-376): model upload, polygonization, mesh download and the scatter into the sparse
+    21.5-KB-per-MPU PolyMPUs layout.  `poly` is the drop-in's engine: the default 2-part group
+    of psgpu::Polygonize / gpu.Polygonize (a gpu.Group) or one context (gpu.Polygonizer).  C3
+    has 50,653 MPUs, past the reference's MAX_MPU_COUNT (24,000), so its PolyMPUs array is
+    allocated with room for them (1.09 GB).  Median over `reps` calls after 2 warm-ups."""
     from parsip_amd import soa
 
-    model, cs, n = synth.make_config("C2")
-    out = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
+    model, cs, n = synth.make_config(config)
+    ct_need = gpu.count_mpus(cs, *model.bbox)
+    out = np.zeros(max(soa.MAX_MPU_COUNT, ct_need), soa.MPU_DTYPE)
     for _ in range(2):
         rc, ct, _ = poly.polygonize_mpus(cs, model, out)
-        assert rc == 1 and ct == gpu.count_mpus(cs, *model.bbox), (rc, ct)
+        assert rc == 1 and ct == ct_need, (rc, ct)
     t = []
     for _ in range(reps):
         t0 = time.perf_counter()
         poly.polygonize_mpus(cs, model, out)
         t.append(time.perf_counter() - t0)
     med = float(np.median(t))
-    return {"config": f"C2: {model.ct_prims}-prim BlobTree, {n}^3 cells, {ct} MPUs", "ms": round(med * 1e3, 3),
-            "best_ms": round(min(t) * 1e3, 3), "mcells_per_s": round(n ** 3 / med / 1e6, 2),
-            "note": "psgpu_polygonize_mpus end to end (SoA upload, 4 kernels, compact-mesh download over PCIe, "
-                    "host scatter into PolyMPUs); never the bench value"}
+    engine = (f"psgpu_group_polygonize_mpus over {poly.n} parts of one device (the drop-in's default)"
+              if isinstance(poly, gpu.Group) else "psgpu_polygonize_mpus on one context")
+    return {"config": f"{config}: {model.ct_prims}-prim BlobTree, {n}^3 cells, {ct} MPUs", "ms": round(med * 1e3, 3),
+            "best_ms": round(min(t) * 1e3, 3), "mcells_per_s": round(n ** 3 / med / 1e6, 2), "engine": engine,
+            "note": "end to end (SoA upload, the kernel chains, compact-mesh download over PCIe, host scatter into "
+                    "PolyMPUs); never the bench value"}
 
 
 class Engine:
@@ -871,7 +877,15 @@ def main():
                                     "note": "one engine, one polygonization at a time, host-timed "
                                             "(enqueue + kernel chain + sync): a blocking caller's latency"}
         out["latency_ms_single_parts"] = latency_single_parts(device, model, cs, args.jit)
-        out["blocking_polygonize_mpus"] = blocking_contract(poly)
+        bg = gpu.Group([device, device])
+        try:
+            bg.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+            bg.set_option(gpu.OPT_JIT, args.jit)
+            out["blocking_polygonize_mpus"] = blocking_contract(bg, "C2")
+            out["blocking_polygonize_mpus_c3"] = blocking_contract(bg, "C3")
+        finally:
+            bg.close()
+        out["blocking_polygonize_mpus_one_context"] = blocking_contract(poly, "C2")
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3, args.config)
     if grp.rank == 0:

@@ -46,6 +46,9 @@ inline C* as_c_mut(T& v) {
 struct CtxDeleter {
     void operator()(psgpu_ctx* c) const { psgpu_destroy(c); }
 };
+struct GroupDeleter {
+    void operator()(psgpu_group* g) const { psgpu_group_destroy(g); }
+};
 }  // namespace detail
 
 /* One device context (device-resident model and mesh buffers). */
@@ -65,11 +68,41 @@ private:
     int status_ = PSGPU_RET_DEVICE_ERROR;
 };
 
+/* `parts` contexts on one device, each polygonizing a cost-balanced MPU range on a stream of
+ * its own (psgpu_group over {device, ..., device}): a blocking caller's one polygonization
+ * finishes sooner as 2 parts, whose kernel chains fill each other's tails (C3: 0.104 vs
+ * 0.118 ms); the parts' meshes concatenate in range order to the one-context
+ * mesh.  The split comes from a planning run of the lattice (PSGPU_GROUP_BALANCE_PLAN),
+ * made once per cell size and scene box. */
+class Group {
+public:
+    explicit Group(int device = 0, int parts = 2) {
+        std::vector<int> devs((size_t)(parts > 0 ? parts : 1), device);
+        psgpu_group* g = nullptr;
+        status_ = psgpu_group_create(devs.data(), (int)devs.size(), &g);
+        g_.reset(g);
+        if (ok()) status_ = psgpu_group_set_option(g, PSGPU_GROUP_OPT_BALANCE, PSGPU_GROUP_BALANCE_PLAN);
+    }
+    bool ok() const { return g_ != nullptr && status_ == PSGPU_RET_SUCCESS; }
+    int status() const { return status_; }
+    psgpu_group* get() const { return g_.get(); }
+
+private:
+    std::unique_ptr<psgpu_group, detail::GroupDeleter> g_;
+    int status_ = PSGPU_RET_DEVICE_ERROR;
+};
+
 /* The calling thread's default context on device 0 (the reference's Polygonize is a
  * free function with process-global state, PS_Polygonizer.cpp:18-19). */
 inline Context& default_context() {
     static thread_local Context ctx(0);
     return ctx;
+}
+
+/* The calling thread's default blocking group: 2 parts on device 0. */
+inline Group& default_group() {
+    static thread_local Group g(0, 2);
+    return g;
 }
 
 /* CountMPUNeeded (PS_Polygonizer.h:384). */
@@ -89,20 +122,30 @@ inline int PrepareBBoxes(float cellsize, Prims& prims, BoxMats& boxMatrices, Ops
 
 /* Polygonize (PS_Polygonizer.h:386-391): fills polyMPUs.vMPUs[0..ctMPUs) and ctMPUs.
  * PolyMPUs is {MPU vMPUs[MAX_MPU_COUNT]; U32 ctMPUs;} (PS_Polygonizer.h:196-198);
- * MPUs that fail S1 get zero counts (the reference leaves them stale). */
+ * MPUs that fail S1 get zero counts (the reference leaves them stale).  Without `ctx` it
+ * runs on the calling thread's default 2-part group (default_group(): the shortest wait
+ * for one polygonization); with `ctx`, on that one context. */
 template <class Prims, class Mats, class Ops, class PolyMPUsT>
 inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
                       void* lpProcessStats = nullptr, Context* ctx = nullptr) {
     static_assert(sizeof(polyMPUs.vMPUs[0]) == sizeof(PsMPU), "MPU layout");
     (void)lpProcessStats;  // MPUSTATS is filled by the reference only under a compile flag
-    Context& c = ctx ? *ctx : default_context();
-    if (!c.ok()) return c.status();
     const uint32_t capacity = (uint32_t)(sizeof(polyMPUs.vMPUs) / sizeof(polyMPUs.vMPUs[0]));
     uint32_t ct = 0;
-    const int rc = psgpu_polygonize_mpus(c.get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
+    int rc;
+    if (ctx) {
+        if (!ctx->ok()) return ctx->status();
+        rc = psgpu_polygonize_mpus(ctx->get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
+                                   detail::as_c<Mats, PsSoaPrimMatrices>(mats), detail::as_c<Ops, PsSoaBlobOps>(ops),
+                                   reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr);
+    } else {
+        Group& g = default_group();
+        if (!g.ok()) return g.status();
+        rc = psgpu_group_polygonize_mpus(g.get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
                                          detail::as_c<Mats, PsSoaPrimMatrices>(mats),
                                          detail::as_c<Ops, PsSoaBlobOps>(ops),
-                                         reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr);
+                                         reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct);
+    }
     // on failure nothing was exported: report no MPUs (SimdPoly::draw walks ctMPUs,
     // PS_HighPerformanceRender.cpp:378-426, and must not draw stale ones)
     polyMPUs.ctMPUs = rc == PSGPU_RET_SUCCESS ? ct : 0u;
@@ -170,8 +213,11 @@ public:
     static constexpr int kErrOperatorOverflow = -2;  // PS_ERROR_OPERATOR_OVERFLOW
     static constexpr int kErrNonBinaryOp = -3;       // PS_ERROR_NON_BINARY_OP
 
-    explicit SimdPolyT(int device = 0, bool translateTypes = true, bool triangleCompat = false)
-        : ctx_(device), translate_(translateTypes), triangleCompat_(triangleCompat) {
+    /* `parts`: the polygonization runs as that many cost-balanced MPU ranges on streams of
+     * the device (Group; 2 by default: run() waits for one polygonization, and 2 parts
+     * finish it sooner than one context) */
+    explicit SimdPolyT(int device = 0, bool translateTypes = true, bool triangleCompat = false, int parts = 2)
+        : grp_(device, parts), translate_(translateTypes), triangleCompat_(triangleCompat) {
         reset();
     }
 
@@ -196,11 +242,11 @@ public:
     /* SimdPoly::run (.cpp:373-376): upload the SoA and polygonize on the device (blocking;
      * the compact mesh stays in HBM until draw / exportPolyMPUs / mesh). */
     int run(float cellsize) {
-        if (!ctx_.ok()) return ctx_.status();
+        if (!grp_.ok()) return grp_.status();
         if (prims_.ctPrims == 0) return PSGPU_RET_PARAM_ERROR;  // Polygonize :322-323
-        int rc = psgpu_set_model(ctx_.get(), &prims_, &primMats_, &ops_);
-        if (rc == PSGPU_RET_SUCCESS) rc = psgpu_polygonize(ctx_.get(), cellsize, 0, 0xffffffffu, nullptr);
-        if (rc == PSGPU_RET_SUCCESS) rc = psgpu_finish(ctx_.get(), &info_);
+        int rc = psgpu_group_set_model(grp_.get(), &prims_, &primMats_, &ops_);
+        if (rc == PSGPU_RET_SUCCESS) rc = psgpu_group_polygonize(grp_.get(), cellsize);
+        if (rc == PSGPU_RET_SUCCESS) rc = psgpu_group_finish(grp_.get(), &info_, nullptr);
         haveMesh_ = false;
         return rc;
     }
@@ -231,18 +277,20 @@ public:
         static_assert(sizeof(polyMPUs.vMPUs[0]) == sizeof(PsMPU), "MPU layout");
         const uint32_t capacity = (uint32_t)(sizeof(polyMPUs.vMPUs) / sizeof(polyMPUs.vMPUs[0]));
         uint32_t ct = 0;
-        const int rc = psgpu_export_polympus(ctx_.get(), reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct);
+        const int rc =
+            psgpu_group_export_polympus(grp_.get(), reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct);
         polyMPUs.ctMPUs = rc == PSGPU_RET_SUCCESS ? ct : 0u;
         return rc;
     }
 
-    int mesh(PsMeshDevice* out) { return psgpu_mesh_device(ctx_.get(), out); }
+    /* the whole mesh in HBM of the device (the parts gathered, vertex ids rebased) */
+    int mesh(PsMeshDevice* out) { return psgpu_group_gather(grp_.get(), 0, out); }
     const PsMeshInfo& info() const { return info_; }
     const PsSoaBlobPrims& prims() const { return prims_; }
     const PsSoaBlobOps& ops() const { return ops_; }
     const PsSoaPrimMatrices& primMatrices() const { return primMats_; }
     const PsSoaBoxMatrices& boxMatrices() const { return boxMats_; }
-    Context& context() { return ctx_; }
+    Group& group() { return grp_; }
 
 private:
     template <class V>
@@ -411,7 +459,7 @@ private:
     int download() {
         if (haveMesh_) return PSGPU_RET_SUCCESS;
         PsMeshInfo I;
-        int rc = psgpu_finish(ctx_.get(), &I);
+        int rc = psgpu_group_finish(grp_.get(), &I, nullptr);
         if (rc != PSGPU_RET_SUCCESS) return rc;
         info_ = I;
         pos_.resize((size_t)I.ctVertices * 3);
@@ -419,12 +467,12 @@ private:
         col_.resize(pos_.size());
         tris_.resize((size_t)I.ctTriangles * 3);
         offs_.resize((size_t)I.ctMPUs + 1);
-        rc = psgpu_download_mesh(ctx_.get(), pos_.data(), nrm_.data(), col_.data(), tris_.data(), offs_.data());
+        rc = psgpu_group_download_mesh(grp_.get(), pos_.data(), nrm_.data(), col_.data(), tris_.data(), offs_.data());
         haveMesh_ = rc == PSGPU_RET_SUCCESS;
         return rc;
     }
 
-    Context ctx_;
+    Group grp_;
     bool translate_, triangleCompat_;
     PsSoaBlobPrims prims_;
     PsSoaBlobOps ops_;

@@ -892,23 +892,24 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     base = lane_value(base, 0);
     if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u))] = mOf;
     phase_stamp(p, 3, 8192u);
-    // Culling masks of each queued MPU, from this wave's culling segments (already in
-    // registers): its box for S2 (with the queue entry: k_mpu loads no culling data) and the
-    // box grown by the normal delta for k_vertex / k_finish
+    // Culling mask of each queued MPU, from this wave's culling segments (already in
+    // registers): its box grown by the normal delta, for k_vertex / k_finish (mpuMasks) and,
+    // with the queue entry, for S2 (k_mpu loads no culling data).  The grown box contains the
+    // S2 box, so its mask is conservative there too; one mask per MPU instead of two (the
+    // boxes differ by 0.001: the masks are the same but for primitives grazing the box).
     if (p.cull) {
-        const float e = 7.0f * p.cs, eg = 7.0f * p.cs + 0.001f;
+        const float eg = 7.0f * p.cs + 0.001f;
         for (uint32_t qm = queue8; qm != 0u; qm &= qm - 1u) {
             const int q = __builtin_ctz(qm);
             const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[0]), 8 * q));
             const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[1]), 8 * q));
             const float oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[2]), 8 * q));
-            const CullMask a = cull_mask_from(cl, ox, oy, oz, ox + e, oy + e, oz + e);
             const CullMask g = cull_mask_from(cl, ox, oy, oz, ox + eg, oy + eg, oz + eg);
             const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << q) - 1u));
             const uint32_t wq = lane_value(mOf, q) - p.mpuBegin;
             if (lane == 0) {
-                p.pqMask[2 * slotq] = a.lo;
-                p.pqMask[2 * slotq + 1] = a.hi;
+                p.pqMask[2 * slotq] = g.lo;
+                p.pqMask[2 * slotq + 1] = g.hi;
                 p.mpuMasks[2 * wq] = g.lo;
                 p.mpuMasks[2 * wq + 1] = g.hi;
             }

@@ -436,12 +436,20 @@ int psgpu_group_export_polympus(psgpu_group* g, PsMPU* mpus, uint32_t capacity, 
     if (T.ctMPUs > capacity) return PSGPU_RET_MPU_OVERFLOW;
     if (T.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
     if (!mpus) return PSGPU_RET_PARAM_ERROR;
+    // every part's copies first (each on its own stream), then the scatters in range order:
+    // the later parts' downloads overlap the earlier parts' scatter
+    std::vector<ExportStage> st(g->parts.size());
+    for (size_t p = 0; p < g->parts.size(); ++p) {
+        rc = set_device(g->parts[p]);
+        if (rc == PSGPU_RET_SUCCESS) rc = export_stage(g->parts[p], true, false, &st[p]);
+        if (rc != PSGPU_RET_SUCCESS) return rc;
+    }
     uint32_t at = 0;
     for (size_t p = 0; p < g->parts.size(); ++p) {
-        uint32_t ct = 0;
-        rc = psgpu_export_polympus(g->parts[p], mpus + at, capacity - at, &ct);
+        rc = set_device(g->parts[p]);
+        if (rc == PSGPU_RET_SUCCESS) rc = export_scatter(g->parts[p], st[p], mpus + at, nullptr);
         if (rc != PSGPU_RET_SUCCESS) return rc;
-        at += ct;
+        at += g->parts[p]->mpuCount;
     }
     return PSGPU_RET_SUCCESS;
 }

@@ -1381,26 +1381,32 @@ int psgpu_split_costs(const uint32_t* costs, uint32_t n, uint32_t parts, uint32_
     return PSGPU_RET_SUCCESS;
 }
 
-namespace {
+}  // extern "C"
+
+namespace psgpu {
 // The blocking export (Polygonize :360-371 into PolyMPUs, and the MPUSTATS of :372-376): one
 // batch of async copies of the compact mesh, offsets, S1 flags and (for stats) counts into the
-// context's pinned staging buffer, one wait, then the host scatter.  Pageable destinations
-// would cost a staged copy and a wait each (7 of them for a mesh plus statistics).
-int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt, PsMpuStats* stats) {
-    PsMeshInfo I;
-    int rc = psgpu_finish(c, &I);
-    if (rc != PSGPU_RET_SUCCESS) return rc;
-    if (outCt) *outCt = c->mpuCount;
-    if (mpus) {
-        if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
-        if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
-    }
-    if (!mpus && !stats) return PSGPU_RET_PARAM_ERROR;
-    const size_t V = mpus ? I.ctVertices : 0, T = mpus ? I.ctTriangles : 0, N = c->mpuCount;
+// context's pinned staging buffer (export_stage), one wait, then the host scatter
+// (export_scatter).  Pageable destinations would cost a staged copy and a wait each (7 of
+// them for a mesh plus statistics).  A group stages every part before it scatters the first,
+// so the later parts' copies overlap the earlier parts' scatter.  Call after psgpu_finish.
+int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
+    const PsMeshInfo& I = c->info;
+    ExportStage& S = *st;
+    S.mesh = mesh;
+    S.stats = stats;
+    S.V = mesh ? I.ctVertices : 0;
+    S.T = mesh ? I.ctTriangles : 0;
+    S.N = c->mpuCount;
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t oOffs = 0, oPos = up(oOffs + (N + 1) * 8), oNrm = up(oPos + V * 12), oCol = up(oNrm + V * 12),
-                 oTris = up(oCol + V * 12), oPass = up(oTris + T * 12), oCnt = up(oPass + N),
-                 total = up(oCnt + (stats ? N * 8 : 0));
+    S.oOffs = 0;
+    S.oPos = up(S.oOffs + (S.N + 1) * 8);
+    S.oNrm = up(S.oPos + S.V * 12);
+    S.oCol = up(S.oNrm + S.V * 12);
+    S.oTris = up(S.oCol + S.V * 12);
+    S.oPass = up(S.oTris + S.T * 12);
+    S.oCnt = up(S.oPass + S.N);
+    const size_t total = up(S.oCnt + (stats ? S.N * 8 : 0));
     if (total > c->hostStageCap) {
         if (c->hostStage) (void)hipHostFree(c->hostStage);
         c->hostStage = nullptr;
@@ -1411,25 +1417,32 @@ int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outC
     }
     unsigned char* h = c->hostStage;
     hipStream_t s = c->stream;
+    const size_t N = S.N, V = S.V, T = S.T;
     if (N) {
-        if (mpus) PSGPU_CHECK(hipMemcpyAsync(h + oOffs, c->offs, (N + 1) * 8, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipMemcpyAsync(h + oPass, c->passed, N, hipMemcpyDeviceToHost, s));
-        if (stats) PSGPU_CHECK(hipMemcpyAsync(h + oCnt, c->counts, N * 8, hipMemcpyDeviceToHost, s));
+        if (mesh) PSGPU_CHECK(hipMemcpyAsync(h + S.oOffs, c->offs, (N + 1) * 8, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + S.oPass, c->passed, N, hipMemcpyDeviceToHost, s));
+        if (stats) PSGPU_CHECK(hipMemcpyAsync(h + S.oCnt, c->counts, N * 8, hipMemcpyDeviceToHost, s));
     }
     if (V) {
-        PSGPU_CHECK(hipMemcpyAsync(h + oPos, c->pos, V * 12, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipMemcpyAsync(h + oNrm, c->nrm, V * 12, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipMemcpyAsync(h + oCol, c->col, V * 12, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + S.oPos, c->pos, V * 12, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + S.oNrm, c->nrm, V * 12, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipMemcpyAsync(h + S.oCol, c->col, V * 12, hipMemcpyDeviceToHost, s));
     }
-    if (T) PSGPU_CHECK(hipMemcpyAsync(h + oTris, c->tris, T * 12, hipMemcpyDeviceToHost, s));
-    PSGPU_CHECK(hipStreamSynchronize(s));
-    const uint64_t* off = reinterpret_cast<const uint64_t*>(h + oOffs);
-    const float* pos = reinterpret_cast<const float*>(h + oPos);
-    const float* nrm = reinterpret_cast<const float*>(h + oNrm);
-    const float* col = reinterpret_cast<const float*>(h + oCol);
-    const uint32_t* tris = reinterpret_cast<const uint32_t*>(h + oTris);
-    const uint8_t* passed = h + oPass;
-    if (mpus) {
+    if (T) PSGPU_CHECK(hipMemcpyAsync(h + S.oTris, c->tris, T * 12, hipMemcpyDeviceToHost, s));
+    return PSGPU_RET_SUCCESS;
+}
+
+int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats) {
+    PSGPU_CHECK(hipStreamSynchronize(c->stream));
+    const unsigned char* h = c->hostStage;
+    const size_t N = S.N, V = S.V, T = S.T;
+    const uint64_t* off = reinterpret_cast<const uint64_t*>(h + S.oOffs);
+    const float* pos = reinterpret_cast<const float*>(h + S.oPos);
+    const float* nrm = reinterpret_cast<const float*>(h + S.oNrm);
+    const float* col = reinterpret_cast<const float*>(h + S.oCol);
+    const uint32_t* tris = reinterpret_cast<const uint32_t*>(h + S.oTris);
+    const uint8_t* passed = h + S.oPass;
+    if (mpus && S.mesh) {
         const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
         // the scatter is bound by the write-allocates of the sparse PolyMPUs layout (21.5 KB per
         // MPU): several host threads, as the reference's TBB bodies fill it
@@ -1474,8 +1487,8 @@ int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outC
             for (std::thread& t : th) t.join();
         }
     }
-    if (stats) {
-        const uint64_t* cnt = reinterpret_cast<const uint64_t*>(h + oCnt);
+    if (stats && S.stats) {
+        const uint64_t* cnt = reinterpret_cast<const uint64_t*>(h + S.oCnt);
         memset(stats, 0, sizeof(PsMpuStats) * N);
         for (uint32_t l = 0; l < N; ++l) {
             PsMpuStats& st = stats[l];
@@ -1489,7 +1502,27 @@ int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outC
     }
     return PSGPU_RET_SUCCESS;
 }
+}  // namespace psgpu
+
+namespace {
+int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt, PsMpuStats* stats) {
+    PsMeshInfo I;
+    int rc = psgpu_finish(c, &I);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (outCt) *outCt = c->mpuCount;
+    if (mpus) {
+        if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
+        if (I.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
+    }
+    if (!mpus && !stats) return PSGPU_RET_PARAM_ERROR;
+    ExportStage st;
+    rc = export_stage(c, mpus != nullptr, stats != nullptr, &st);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    return export_scatter(c, st, mpus, stats);
+}
 }  // namespace
+
+extern "C" {
 
 int psgpu_export_polympus(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt) {
     if (!mpus) {  // the count (and overflow) check alone

@@ -133,6 +133,16 @@ namespace psgpu {
 int hip_fail(hipError_t e, const char* what);
 // Make the context's device current on the calling thread.
 int set_device(psgpu_ctx* c);
+// The blocking export of a finished run in two steps (psgpu_host.cpp): enqueue the copies of
+// the compact mesh (mesh), the S1 flags and (stats) the per-MPU counts into the context's
+// pinned staging buffer, then wait and scatter into PolyMPUs / PsMpuStats.
+struct ExportStage {
+    bool mesh = false, stats = false;
+    size_t V = 0, T = 0, N = 0;
+    size_t oOffs = 0, oPos = 0, oNrm = 0, oCol = 0, oTris = 0, oPass = 0, oCnt = 0;
+};
+int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st);
+int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats);
 }  // namespace psgpu
 
 #define PSGPU_CHECK(expr)                                           \

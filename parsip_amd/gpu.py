@@ -408,10 +408,11 @@ class Polygonizer:
         of start, end (100 MHz ticks), item | hw id << 32, launched waves only."""
         return _stamps(self._L, self._ctx)
 
-    def spans(self) -> np.ndarray:
+    def spans(self, raw: bool = False) -> np.ndarray:
         """(runs, kernels) device-clock kernel spans in ms of the runs recorded since
-        OPT_SPANS was set (kernels in STAMP_KERNELS order)."""
-        return _spans(self._L, self._ctx)
+        OPT_SPANS was set (kernels in STAMP_KERNELS order); raw: (runs, kernels, 2) start /
+        end ticks of the 100 MHz device clock."""
+        return _spans(self._L, self._ctx, raw)
 
     def kernel_times(self) -> dict:
         """Per-kernel hipEvent times (ms) of the last finished run (OPT_KERNEL_TIMING)."""
@@ -436,13 +437,22 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
     """Blocking drop-in for PS::SIMDPOLY::Polygonize.
 
     Fills ``poly_mpus`` (a MPU_DTYPE array, default capacity MAX_MPU_COUNT as in PolyMPUs)
-    and returns ``(code, ctMPUs, poly_mpus)``.
+    and returns ``(code, ctMPUs, poly_mpus)``.  Runs on this process's default 2-part group
+    of the device (the shortest wait for one polygonization, as parsip_gpu.hpp's
+    psgpu::Polygonize); with ``stats`` (per-MPU PsMpuStats) on one context.
     """
     if model.ct_prims == 0:
         return soa.RET_PARAM_ERROR, 0, poly_mpus
-    if device not in _DEFAULT:
-        _DEFAULT[device] = Polygonizer(device)
-    return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats)
+    if stats is not None:
+        if device not in _DEFAULT:
+            _DEFAULT[device] = Polygonizer(device)
+        return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats)
+    key = ("group", device)
+    if key not in _DEFAULT:
+        g = Group([device, device])
+        g.set_option(GROUP_OPT_BALANCE, BALANCE_PLAN)
+        _DEFAULT[key] = g
+    return _DEFAULT[key].polygonize_mpus(cellsize, model, poly_mpus)
 
 
 def _mesh_from_arrays(V, T, N, fill):
@@ -539,6 +549,18 @@ class Group:
                "psgpu_group_export_polympus")
         return out[:ct.value]
 
+    def polygonize_mpus(self, cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None = None):
+        """psgpu_group_polygonize_mpus: the reference's blocking Polygonize over the group's
+        parts (model upload, run, download and scatter into the caller's PolyMPUs).
+        Returns ``(code, ctMPUs, poly_mpus)``."""
+        if poly_mpus is None:
+            poly_mpus = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
+        ct = ctypes.c_uint32()
+        p, m, o = model.ptrs()
+        rc = self._L.psgpu_group_polygonize_mpus(self._g, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
+                                                 ctypes.byref(ct))
+        return rc, ct.value, poly_mpus
+
     def context_ptr(self, part: int):
         return self._L.psgpu_group_context(self._g, part)
 
@@ -567,12 +589,14 @@ def _stamps(L, ctx) -> dict:
     return out
 
 
-def _spans(L, ctx) -> np.ndarray:
+def _spans(L, ctx, raw: bool = False) -> np.ndarray:
     runs = ctypes.c_uint32()
     _check(L.psgpu_download_spans(ctx, None, ctypes.byref(runs)), "psgpu_download_spans")
     out = np.zeros((max(runs.value, 1), len(STAMP_KERNELS), 2), np.uint64)
     _check(L.psgpu_download_spans(ctx, out.ctypes.data, ctypes.byref(runs)), "psgpu_download_spans")
     out = out[:runs.value].astype(np.int64)
+    if raw:  # (runs, kernels, {first wave start, last wave end}) in 100 MHz device ticks
+        return out
     return (out[:, :, 1] - out[:, :, 0]) * 1e-5  # (runs, kernels) in ms (100 MHz ticks)
 
 
