@@ -880,6 +880,7 @@ def main():
         bg = gpu.Group([device, device])
         try:
             bg.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+            bg.set_option(gpu.GROUP_OPT_MIN_PART_MPUS, gpu.BLOCKING_MIN_PART_MPUS)  # as the drop-ins
             bg.set_option(gpu.OPT_JIT, args.jit)
             out["blocking_polygonize_mpus"] = blocking_contract(bg, "C2")
             out["blocking_polygonize_mpus_c3"] = blocking_contract(bg, "C3")

@@ -346,6 +346,10 @@ typedef struct PsGroupPart {
 #define PSGPU_GROUP_BALANCE_EVERY_RUN   2 /* plan, then re-split after every finish from
                                              the costs of that run (animations)          */
 #define PSGPU_GROUP_BALANCE_FIXED       3 /* the split of psgpu_group_set_split          */
+#define PSGPU_GROUP_OPT_MIN_PART_MPUS 101 /* 0 (default): every part gets a range; n > 0:
+                                             only the first max(1, lattice MPUs / n) parts
+                                             do, the others stay empty -- a small lattice
+                                             runs as one chain (EVEN / PLAN / EVERY_RUN) */
 
 /* devices: nParts HIP ordinals (NULL: 0 .. nParts-1). */
 int  psgpu_group_create(const int* devices, int nParts, psgpu_group** out);

@@ -74,14 +74,20 @@ private:
  * 0.118 ms); the parts' meshes concatenate in range order to the one-context
  * mesh.  The split comes from a planning run of the lattice (PSGPU_GROUP_BALANCE_PLAN),
  * made once per cell size and scene box. */
+/* A part's smallest range for the blocking drop-ins: a lattice of fewer than 2 x this many
+ * MPUs runs as one chain (C2, 6,859 MPUs: one context 0.049 ms vs 2 parts 0.058 for the
+ * kernels; C3, 50,653: 0.114 vs 0.105 -- tools/blocking_breakdown.py). */
+constexpr uint32_t kBlockingMinPartMpus = 16384;
+
 class Group {
 public:
-    explicit Group(int device = 0, int parts = 2) {
+    explicit Group(int device = 0, int parts = 2, uint32_t minPartMpus = kBlockingMinPartMpus) {
         std::vector<int> devs((size_t)(parts > 0 ? parts : 1), device);
         psgpu_group* g = nullptr;
         status_ = psgpu_group_create(devs.data(), (int)devs.size(), &g);
         g_.reset(g);
         if (ok()) status_ = psgpu_group_set_option(g, PSGPU_GROUP_OPT_BALANCE, PSGPU_GROUP_BALANCE_PLAN);
+        if (ok()) status_ = psgpu_group_set_option(g, PSGPU_GROUP_OPT_MIN_PART_MPUS, minPartMpus);
     }
     bool ok() const { return g_ != nullptr && status_ == PSGPU_RET_SUCCESS; }
     int status() const { return status_; }

@@ -51,9 +51,18 @@ __device__ __forceinline__ bool quad_any(bool v) {
     return x != 0;
 }
 
+// GROUP 5 is GROUP 4 for the S2 cache (k_mpu): the 4 lanes of a group are 4 z-consecutive
+// corners of one x-slice and one y row, and every point of a lane has the lane's y and z.
+// The generated walk uses that to test a pruned op's box once per op for y and z (the
+// group's z union by one quad OR) and per point for x alone: group_any(X | Y | Z) =
+// X | Y | group_any(Z) when X and Y are the same in the 4 lanes -- the same decisions.
+#ifndef PSGPU_S2_GROUP
+#define PSGPU_S2_GROUP 5  // 4: the generic per-point box test (experiments, PSGPU_JIT_FLAGS)
+#endif
+constexpr int kS2Group = PSGPU_S2_GROUP;
 template <int GROUP>
 __device__ __forceinline__ bool group_any(bool v) {
-    if (GROUP == 4) return quad_any(v);
+    if (GROUP == 4 || GROUP == 5) return quad_any(v);
     return v;
 }
 
@@ -116,6 +125,22 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // Value of a wave-uniform lane (scalar read).
 __device__ __forceinline__ uint32_t lane_value(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+// A value the wave holds in every lane, as a scalar (SGPR): branches on it are scalar, and
+// the compiler sees the uniformity its divergence analysis cannot prove (e.g. anything
+// derived from threadIdx.x >> 6).
+#ifndef PSGPU_UNIFORM_CM
+#define PSGPU_UNIFORM_CM 1  // 0: k_mpu's culling mask in VGPRs (experiments)
+#endif
+#ifndef PSGPU_UNIFORM_WAVE
+#define PSGPU_UNIFORM_WAVE 1  // 0: the wave index as the compiler derives it (experiments)
+#endif
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int wave_index() {
+    return PSGPU_UNIFORM_WAVE ? (int)uniform(threadIdx.x >> 6) : (int)(threadIdx.x >> 6);
+}
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return (uint64_t)uniform((uint32_t)v) | ((uint64_t)uniform((uint32_t)(v >> 32)) << 32);
 }
 
 // ---------------------------------------------------------------------------
@@ -740,7 +765,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wav
 // block reaches both barriers; the second wave of a brick stops after them.
 template <class EV, int SPLIT = 1>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_index();
     const int lane = lane_id();
     const int part = wave % SPLIT;  // subtree of the root this wave walks (SPLIT 2)
     const int slot = wave / SPLIT;  // the block's brick
@@ -971,7 +996,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     *item = 0xffffffffu;
     constexpr int WPM = SPLIT > 1 ? SPLIT : kMpuWaves;  // waves per MPU
     constexpr int MPB = 4 / WPM;                         // MPUs per block
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_index();
     const int lane = lane_id();
     const int slot = wave / WPM;  // the block's MPU this wave works on
     const int part = wave % WPM;  // its share: x-slices [part * NX, part * NX + NX), or a subtree
@@ -1004,11 +1029,17 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     if (live) {
         const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
         const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
-        const uint32_t slotq = pshard * p.pShardCap + pidx;
-        m = __builtin_amdgcn_readfirstlane(p.pq[slotq]);
-        if (p.cull) {  // the MPU box's culling mask, made by k_precheck
+        const uint32_t slotq = uniform(pshard * p.pShardCap + pidx);
+        m = uniform(p.pq[slotq]);
+        if (p.cull) {  // the MPU box's culling mask, made by k_precheck: in SGPRs, so every
+                       // per-primitive culling test of the walk is a scalar branch
+#if PSGPU_UNIFORM_CM
+            cm.lo = uniform64(p.pqMask[2 * slotq]);
+            cm.hi = uniform64(p.pqMask[2 * slotq + 1]);
+#else
             cm.lo = p.pqMask[2 * slotq];
             cm.hi = p.pqMask[2 * slotq + 1];
+#endif
         }
         *item = m;
         w = m - p.mpuBegin;  // slot of the MPU in the range: counts / offsets index
@@ -1042,18 +1073,18 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
             pzs[x] = pz;
         }
         if constexpr (SPLIT > 1) {
-            if (part == 0) ev.template evaln_part<4, false, 8, 0>(pxs, pys, pzs, cm, fs, nullptr);
-            else ev.template evaln_part<4, false, 8, 1>(pxs, pys, pzs, cm, fs, nullptr);
+            if (part == 0) ev.template evaln_part<kS2Group, false, 8, 0>(pxs, pys, pzs, cm, fs, nullptr);
+            else ev.template evaln_part<kS2Group, false, 8, 1>(pxs, pys, pzs, cm, fs, nullptr);
         } else {
 #if PSGPU_S2_N == 1
         // one walk per x-slice in a runtime loop: the walk's code stays resident in the
         // instruction cache (unrolled copies of a 32-primitive walk do not fit)
 #pragma unroll 1
-        for (int h = 0; h < NX; ++h) fs[h] = ev.template eval<4, false>(pxs[h], py, pz, cm, nullptr);
+        for (int h = 0; h < NX; ++h) fs[h] = ev.template eval<kS2Group, false>(pxs[h], py, pz, cm, nullptr);
 #else
 #pragma unroll
         for (int h = 0; h < NX; h += PSGPU_S2_N)
-            ev.template evaln<4, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs + h, nullptr);
+            ev.template evaln<kS2Group, false, PSGPU_S2_N>(pxs + h, pys + h, pzs + h, cm, fs + h, nullptr);
 #endif
         // inside bits of the 8x8x8 corners: ins[x] bit y*8 + z (lane order)
 #pragma unroll
@@ -1492,7 +1523,7 @@ __device__ __forceinline__ void vertex_root(const EdgeSeg& E, uint32_t iv, float
 template <class EV, int VPW = 16>
 __device__ __forceinline__ void vertex_body(const Params& p, float* lds) {
     constexpr int VN = PSGPU_V_N;
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_index();
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
@@ -1607,7 +1638,7 @@ if constexpr (VPW == 64) {
 // grid, e.g. a small rank share; more total work otherwise).  Same values either way.
 template <class EV, int VPW = 64>
 __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_index();
     const int lane = lane_id();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
@@ -1837,7 +1868,7 @@ if constexpr (VPW == 16) {
 template <class EV>
 __device__ __forceinline__ void probe_body(const Params& p, float* lds, const float* xyz, float* out, float* colOut,
                                            uint32_t n, int mode) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_index();
     ModelPtr M = as_const(p.model);
     EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane_id());
     uint32_t i = blockIdx.x * 256 + threadIdx.x;

@@ -37,6 +37,7 @@ struct psgpu_group {
     std::vector<psgpu_ctx*> parts;
     std::vector<uint32_t> bounds;   // parts + 1 global MPU ids
     int balance = 1;                // PSGPU_GROUP_BALANCE_*
+    uint32_t minPartMpus = 0;       // PSGPU_GROUP_OPT_MIN_PART_MPUS
     bool planned = false;           // bounds are a cost split of the current lattice
     float planCs = 0.0f;
     PsVec3f planLo{}, planHi{};
@@ -99,10 +100,18 @@ uint32_t plan_chunk_mpus() {
     return chunk;
 }
 
-void even_split(psgpu_group* g, uint32_t total) {
+// Parts that get a range: all, or with PSGPU_GROUP_OPT_MIN_PART_MPUS the first
+// total / minPartMpus of them (at least one); the rest get empty ranges at the end.
+uint32_t active_parts(const psgpu_group* g, uint32_t total) {
     const uint32_t n = (uint32_t)g->parts.size();
-    g->bounds.assign(n + 1, 0);
-    for (uint32_t k = 0; k <= n; ++k) g->bounds[k] = (uint32_t)((uint64_t)total * k / n);
+    if (!g->minPartMpus) return n;
+    return std::max(1u, std::min(n, total / g->minPartMpus));
+}
+
+void even_split(psgpu_group* g, uint32_t total) {
+    const uint32_t n = (uint32_t)g->parts.size(), a = active_parts(g, total);
+    g->bounds.assign(n + 1, total);
+    for (uint32_t k = 0; k < a; ++k) g->bounds[k] = (uint32_t)((uint64_t)total * k / a);
 }
 
 // Cost split of the lattice from a planning run of the whole grid on part 0 (one
@@ -110,10 +119,10 @@ void even_split(psgpu_group* g, uint32_t total) {
 // results are exact, so every caller that plans the same model and lattice gets the same
 // split).
 int plan(psgpu_group* g, float cs, uint32_t total) {
-    const uint32_t n = (uint32_t)g->parts.size();
-    g->bounds.assign(n + 1, 0);
-    g->bounds[n] = total;
-    if (n > 1 && total > 0) {
+    const uint32_t n = (uint32_t)g->parts.size(), a = active_parts(g, total);
+    g->bounds.assign(n + 1, total);
+    g->bounds[0] = 0;
+    if (a > 1 && total > 0) {
         std::vector<uint32_t> costs(total);
         for (uint32_t b = 0; b < total;) {
             const uint32_t e = (uint32_t)std::min<uint64_t>(total, (uint64_t)b + plan_chunk_mpus());
@@ -123,7 +132,7 @@ int plan(psgpu_group* g, float cs, uint32_t total) {
             if (rc != PSGPU_RET_SUCCESS) return rc;
             b = e;
         }
-        const int rc = psgpu_split_costs(costs.data(), total, n, 0, g->bounds.data());
+        const int rc = psgpu_split_costs(costs.data(), total, a, 0, g->bounds.data());
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
     const PsSoaBlobPrims& P = g->parts[0]->primsHost;
@@ -144,7 +153,9 @@ int replan_from_last(psgpu_group* g) {
         const int rc = psgpu_mpu_costs(g->parts[p], costs.data() + (g->bounds[p] - begin));
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
-    return psgpu_split_costs(costs.data(), total, n, begin, g->bounds.data());
+    const uint32_t a = active_parts(g, total);
+    std::fill(g->bounds.begin(), g->bounds.end(), begin + total);
+    return psgpu_split_costs(costs.data(), total, a, begin, g->bounds.data());
 }
 
 }  // namespace
@@ -206,6 +217,13 @@ int psgpu_group_set_option(psgpu_group* g, int option, int64_t value) {
         if (value < 0 || value > 3) return PSGPU_RET_PARAM_ERROR;
         g->balance = (int)value;
         g->planned = false;
+        return PSGPU_RET_SUCCESS;
+    }
+    if (option == PSGPU_GROUP_OPT_MIN_PART_MPUS) {
+        if (value < 0 || value > 0xffffffffll) return PSGPU_RET_PARAM_ERROR;
+        g->minPartMpus = (uint32_t)value;
+        g->planned = false;
+        g->bounds.clear();  // re-split at the next polygonize
         return PSGPU_RET_SUCCESS;
     }
     for (psgpu_ctx* c : g->parts) {

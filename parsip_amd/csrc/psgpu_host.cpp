@@ -1102,8 +1102,10 @@ int psgpu_set_model(psgpu_ctx* c, const PsSoaBlobPrims* prims, const PsSoaPrimMa
     delete m;
     c->splittable = jit_splittable(c->model);
     memcpy(&c->primsHost, prims, sizeof(PsSoaBlobPrims));
-    PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
-    PSGPU_CHECK(hipStreamSynchronize(c->stream));
+    if (!same) {  // the same bytes are already in HBM (a blocking caller re-sending its model)
+        PSGPU_CHECK(hipMemcpyAsync(c->dModel, &c->model, sizeof(DevModel), hipMemcpyHostToDevice, c->stream));
+        PSGPU_CHECK(hipStreamSynchronize(c->stream));
+    }
     c->haveModel = true;
     if (!same || (!c->jit && !c->jitPending)) jit_start(c);
     return PSGPU_RET_SUCCESS;
@@ -1434,6 +1436,7 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
 
 int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats) {
     PSGPU_CHECK(hipStreamSynchronize(c->stream));
+    if (c->debug & (1 << 22)) return PSGPU_RET_SUCCESS;  // profiling: the copies without the scatter
     const unsigned char* h = c->hostStage;
     const size_t N = S.N, V = S.V, T = S.T;
     const uint64_t* off = reinterpret_cast<const uint64_t*>(h + S.oOffs);

@@ -86,6 +86,8 @@ OPT_TIER_RUNS = 18
 JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values
 STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
+GROUP_OPT_MIN_PART_MPUS = 101
+BLOCKING_MIN_PART_MPUS = 16384  # parsip_gpu.hpp kBlockingMinPartMpus: small lattices run as one chain
 BALANCE_EVEN, BALANCE_PLAN, BALANCE_EVERY_RUN, BALANCE_FIXED = 0, 1, 2, 3
 COMM_ID_BYTES = 128
 
@@ -451,6 +453,7 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
     if key not in _DEFAULT:
         g = Group([device, device])
         g.set_option(GROUP_OPT_BALANCE, BALANCE_PLAN)
+        g.set_option(GROUP_OPT_MIN_PART_MPUS, BLOCKING_MIN_PART_MPUS)
         _DEFAULT[key] = g
     return _DEFAULT[key].polygonize_mpus(cellsize, model, poly_mpus)
 

@@ -120,6 +120,33 @@ def test_group_plan_in_chunks_equals_one_run(gpu_poly, monkeypatch):
         g.close()
 
 
+def test_group_min_part_mpus(oracle):
+    """PSGPU_GROUP_OPT_MIN_PART_MPUS (the blocking drop-ins' 16,384): C2's 6,859 MPUs run as one
+    chain on part 0 (part 1 empty), 2 x 1,000 splits it; the mesh is the oracle's either way."""
+    model, cs, _ = synth.make_config("C2")
+    g = gpu.Group([0, 0])
+    try:
+        g.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+        g.set_option(gpu.GROUP_OPT_MIN_PART_MPUS, gpu.BLOCKING_MIN_PART_MPUS)
+        g.set_model(model)
+        info, parts = g.run(cs)
+        assert [int(x) for x in g.split()] == [0, 6859, 6859]
+        assert parts[1].info.ctMPUs == 0 and info.ctMPUs == 6859
+        om = oracle.polygonize(model, cs, threads=8)
+        assert_mesh_matches(g.download(), np.concatenate(_group_stats(g)), om)
+        g.set_option(gpu.GROUP_OPT_MIN_PART_MPUS, 1000)
+        info, parts = g.run(cs)
+        b = [int(x) for x in g.split()]
+        assert 0 < b[1] < 6859 and b[2] == 6859
+        assert_mesh_matches(g.download(), np.concatenate(_group_stats(g)), om)
+        rc, ct, mpus = g.polygonize_mpus(cs, model)
+        assert rc == soa.RET_SUCCESS and ct == 6859
+        np.testing.assert_array_equal(mpus["ctVertices"][:ct], om.stats[:, 2])
+        np.testing.assert_array_equal(mpus["ctTriangles"][:ct], om.stats[:, 3])
+    finally:
+        g.close()
+
+
 def test_group_fixed_split_with_empty_parts(group8, oracle):
     model, cs, _ = synth.make_config("C2")
     n = gpu.count_mpus(cs, *model.bbox)

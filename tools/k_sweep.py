@@ -9,7 +9,7 @@ import statistics
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = "8"  # as bench.py: every engine on a hardware queue of its own
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
