@@ -1636,6 +1636,24 @@ if constexpr (VPW == 64) {
 // vertex walking its 4 points; VPW 16: a quad of lanes per vertex, one point each (a
 // quarter of the walk per wave: shorter spans when the vertices do not fill the persistent
 // grid, e.g. a small rank share; more total work otherwise).  Same values either way.
+// k_finish's walk over its batches: the first nWaves batches one per wave; after that every
+// nWaves-th (static), or with debug bit 23 whichever batch is next when the wave is free (an
+// atomic per batch on a spare counter word, issued at the top of the current batch and read
+// at its end), so a wave that drew a heavy batch does not draw another.
+struct BatchCursor {
+    bool dyn;
+    uint32_t nWaves;
+    uint32_t* ctr;
+    uint32_t grab = 0;
+    __device__ BatchCursor(const Params& p, uint32_t waves)
+        : dyn((p.debug & (1u << 23)) != 0u), nWaves(waves), ctr(&p.ctr->pad[0]) {}
+    __device__ __forceinline__ void prefetch() {
+        grab = 0;
+        if (dyn && lane_id() == 0) grab = atomicAdd(ctr, 1u);
+    }
+    __device__ __forceinline__ uint32_t next(uint32_t b) const { return dyn ? nWaves + lane_value(grab, 0) : b + nWaves; }
+};
+
 template <class EV, int VPW = 64>
 __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const int wave = wave_index();
@@ -1677,7 +1695,9 @@ if constexpr (VPW == 16) {
     // component j of position, normal and colour
     const ShardBatches sv(sCnt, p.vShardCap, 16);
     const int qj = lane & 3;
-    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+    BatchCursor cur(p, nWaves);
+    for (uint32_t batch = wave0; batch < sv.total; batch = cur.next(batch)) {
+        cur.prefetch();
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
         uint32_t rec = first + (uint32_t)(lane >> 2);
@@ -1729,7 +1749,9 @@ if constexpr (VPW == 16) {
     // partner's two values come over DPP; lane j writes component j, lane 0 also component 2
     const ShardBatches sv(sCnt, p.vShardCap, 32);
     const int pj = lane & 1;
-    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+    BatchCursor cur(p, nWaves);
+    for (uint32_t batch = wave0; batch < sv.total; batch = cur.next(batch)) {
+        cur.prefetch();
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
         uint32_t rec = first + (uint32_t)(lane >> 1);
@@ -1789,7 +1811,9 @@ if constexpr (VPW == 16) {
     }
 } else {
     const ShardBatches sv(sCnt, p.vShardCap, 64);
-    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+    BatchCursor cur(p, nWaves);
+    for (uint32_t batch = wave0; batch < sv.total; batch = cur.next(batch)) {
+        cur.prefetch();
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
         uint32_t rec = first + (uint32_t)lane;

@@ -561,6 +561,19 @@ int vertex_vpw(const psgpu_ctx* c) {
     return (uint64_t)c->lastV > 16u * waves && !c->alone ? 64 : 16;  // a lone run: the quad
 }
 
+// k_mpu's dynamic LDS: its per-MPU tables, or (PSGPU_MPU_BLOCKS_PER_CU=n, experiments) padded
+// to 1/n of the CU's 160 KB so at most n of its blocks are resident per CU
+size_t mpu_lds_launch(const psgpu_ctx* c) {
+    static const long perCu = [] {
+        const char* e = getenv("PSGPU_MPU_BLOCKS_PER_CU");
+        return e ? strtol(e, nullptr, 10) : 0L;
+    }();
+    (void)c;
+    const size_t base = mpu_lds_bytes(0);
+    if (perCu <= 0) return base;
+    return std::max(base, (size_t)(160 * 1024 / perCu) & ~(size_t)255);
+}
+
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
@@ -572,7 +585,7 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
+    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_launch(c), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
