@@ -35,6 +35,22 @@ __device__ __forceinline__ Instr load_instr(ModelPtr M, int pc) {
     return I;
 }
 
+// +0.0f made by an instruction of the block it is written in: the culled branch of the
+// generated walk (`else f = 0`) keeps its zeros instead of the compiler turning them into
+// constants of a phi, which it materialises before the branch, on every path
+// (PSGPU_ZERO_ASM 0: plain constants, experiments).
+#ifndef PSGPU_ZERO_ASM
+#define PSGPU_ZERO_ASM 1
+#endif
+__device__ __forceinline__ float zero_f() {
+#if PSGPU_ZERO_ASM
+    float z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+#else
+    return 0.0f;
+#endif
+}
 __device__ __forceinline__ float max_ref(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float min_ref(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float m01(bool c) { return c ? 1.0f : 0.0f; }
