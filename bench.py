@@ -336,8 +336,13 @@ class Engine:
             self.p = None
             self.obj = gpu.Group([device] * self.parts)
         if args.engines > 1:  # engines share the CUs: half the persistent waves each (1.8 % faster at 4)
-            self.obj.set_option(gpu.OPT_VERTEX_BLOCKS_PER_CU, 8)
-            self.obj.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, 4)
+            self.obj.set_option(gpu.OPT_VERTEX_BLOCKS_PER_CU, args.vertex_blocks or 8)
+            self.obj.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, args.finish_blocks or 4)
+        else:
+            if args.vertex_blocks:
+                self.obj.set_option(gpu.OPT_VERTEX_BLOCKS_PER_CU, args.vertex_blocks)
+            if args.finish_blocks:
+                self.obj.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, args.finish_blocks)
         if poly is None or self.parts > 1:
             if args.no_cull:
                 self.obj.set_option(gpu.OPT_CULLING, 0)
@@ -446,6 +451,8 @@ def main():
                          "launches that queue few MPUs (default: 2 for strong scaling over N > 1 ranks, whose "
                          "shares are small, else 0)")
     ap.add_argument("--debug", type=int, default=0, help=argparse.SUPPRESS)  # profiling ablations only
+    ap.add_argument("--vertex-blocks", type=int, default=0, help=argparse.SUPPRESS)  # persistent grids (experiments)
+    ap.add_argument("--finish-blocks", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -849,7 +856,8 @@ def main():
                    "grid": N, "mpus": n_mpus, "prims": model.ct_prims, "ops": model.ct_ops,
                    "parallelism": f"{scaling}-{grp.world}gpu", "engines_per_gpu": neng, "parts_per_engine": nparts,
                    "streams_per_gpu": neng * nparts,
-                   "persistent_blocks_per_cu": [8, 4] if neng > 1 else [16, 8], "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                   "persistent_blocks_per_cu": [args.vertex_blocks or (8 if neng > 1 else 16),
+                                                args.finish_blocks or (4 if neng > 1 else 8)], "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                    "step": "one complete polygonization of the rank's MPU range (all four kernels); steps "
                            "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
