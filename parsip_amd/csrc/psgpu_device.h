@@ -40,7 +40,7 @@ __device__ __forceinline__ Instr load_instr(ModelPtr M, int pc) {
 // constants of a phi, which it materialises before the branch, on every path
 // (PSGPU_ZERO_ASM 0: plain constants, experiments).
 #ifndef PSGPU_ZERO_ASM
-#define PSGPU_ZERO_ASM 1
+#define PSGPU_ZERO_ASM 0  // 1: isolated k_precheck / k_vertex 1-1.5 us slower, 4 engines 2 % slower (r04 A/B)
 #endif
 __device__ __forceinline__ float zero_f() {
 #if PSGPU_ZERO_ASM
@@ -73,7 +73,9 @@ __device__ __forceinline__ bool quad_any(bool v) {
 // group's z union by one quad OR) and per point for x alone: group_any(X | Y | Z) =
 // X | Y | group_any(Z) when X and Y are the same in the 4 lanes -- the same decisions.
 #ifndef PSGPU_S2_GROUP
-#define PSGPU_S2_GROUP 5  // 4: the generic per-point box test (experiments, PSGPU_JIT_FLAGS)
+#define PSGPU_S2_GROUP 4  // 5: the per-op y/z test -- isolated k_mpu 32.3 vs 35.1 us, but four engines
+                          // in flight 0.0611-0.0624 vs 0.0555-0.0560 ms/step (r04 A/B,
+                          // profiles/r04_kernel_variants_ab.txt): kept as an experiment
 #endif
 constexpr int kS2Group = PSGPU_S2_GROUP;
 template <int GROUP>
@@ -149,7 +151,8 @@ __device__ __forceinline__ uint32_t lane_value(uint32_t v, int lane) {
 #define PSGPU_UNIFORM_CM 1  // 0: k_mpu's culling mask in VGPRs (experiments)
 #endif
 #ifndef PSGPU_UNIFORM_WAVE
-#define PSGPU_UNIFORM_WAVE 1  // 0: the wave index as the compiler derives it (experiments)
+#define PSGPU_UNIFORM_WAVE 0  // 1: the wave index through readfirstlane -- 2 % slower with four
+                              // engines (r04 A/B); kept as an experiment
 #endif
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ int wave_index() {
@@ -1652,24 +1655,6 @@ if constexpr (VPW == 64) {
 // vertex walking its 4 points; VPW 16: a quad of lanes per vertex, one point each (a
 // quarter of the walk per wave: shorter spans when the vertices do not fill the persistent
 // grid, e.g. a small rank share; more total work otherwise).  Same values either way.
-// k_finish's walk over its batches: the first nWaves batches one per wave; after that every
-// nWaves-th (static), or with debug bit 23 whichever batch is next when the wave is free (an
-// atomic per batch on a spare counter word, issued at the top of the current batch and read
-// at its end), so a wave that drew a heavy batch does not draw another.
-struct BatchCursor {
-    bool dyn;
-    uint32_t nWaves;
-    uint32_t* ctr;
-    uint32_t grab = 0;
-    __device__ BatchCursor(const Params& p, uint32_t waves)
-        : dyn((p.debug & (1u << 23)) != 0u), nWaves(waves), ctr(&p.ctr->pad[0]) {}
-    __device__ __forceinline__ void prefetch() {
-        grab = 0;
-        if (dyn && lane_id() == 0) grab = atomicAdd(ctr, 1u);
-    }
-    __device__ __forceinline__ uint32_t next(uint32_t b) const { return dyn ? nWaves + lane_value(grab, 0) : b + nWaves; }
-};
-
 template <class EV, int VPW = 64>
 __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const int wave = wave_index();
@@ -1711,9 +1696,7 @@ if constexpr (VPW == 16) {
     // component j of position, normal and colour
     const ShardBatches sv(sCnt, p.vShardCap, 16);
     const int qj = lane & 3;
-    BatchCursor cur(p, nWaves);
-    for (uint32_t batch = wave0; batch < sv.total; batch = cur.next(batch)) {
-        cur.prefetch();
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
         uint32_t rec = first + (uint32_t)(lane >> 2);
@@ -1765,9 +1748,7 @@ if constexpr (VPW == 16) {
     // partner's two values come over DPP; lane j writes component j, lane 0 also component 2
     const ShardBatches sv(sCnt, p.vShardCap, 32);
     const int pj = lane & 1;
-    BatchCursor cur(p, nWaves);
-    for (uint32_t batch = wave0; batch < sv.total; batch = cur.next(batch)) {
-        cur.prefetch();
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
         uint32_t rec = first + (uint32_t)(lane >> 1);
@@ -1827,9 +1808,7 @@ if constexpr (VPW == 16) {
     }
 } else {
     const ShardBatches sv(sCnt, p.vShardCap, 64);
-    BatchCursor cur(p, nWaves);
-    for (uint32_t batch = wave0; batch < sv.total; batch = cur.next(batch)) {
-        cur.prefetch();
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
         uint32_t shard, first, count;
         sv.locate(batch, &shard, &first, &count);
         uint32_t rec = first + (uint32_t)lane;

@@ -92,32 +92,6 @@ def test_finish_layouts_golden(gpu_poly, name, jit):
         gpu_poly.set_option(gpu.OPT_JIT, 1)
 
 
-@pytest.mark.parametrize("jit", [0, 1])
-def test_finish_dynamic_batches_golden(gpu_poly, jit):
-    """k_finish's batches past the first round taken from an atomic counter (debug bit 23)
-    instead of every nWaves-th, in each layout: with one persistent block per CU C3's 5,310
-    64-vertex batches take ~5 rounds of the 1,024 waves; the mesh is the committed oracle's."""
-    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))["C3"]
-    model, cs, _ = synth.make_config("C3")
-    gpu_poly.set_option(gpu.OPT_JIT, jit)
-    gpu_poly.set_model(model)
-    try:
-        gpu_poly.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, 1)
-        for mode in (0, 1, 3, 0):  # 64, 16 and 32 vertices per wave
-            gpu_poly.set_option(gpu.OPT_FINISH_QUAD, mode)
-            gpu_poly.set_option(gpu.OPT_DEBUG, 1 << 23)
-            gpu_poly.run(cs)
-            gm, gs = gpu_poly.download(), gpu_poly.stats()
-            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
-            assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig, (jit, mode)
-    finally:
-        gpu_poly.set_option(gpu.OPT_DEBUG, 0)
-        gpu_poly.set_option(gpu.OPT_FINISH_QUAD, 2)
-        gpu_poly.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, 8)
-        gpu_poly.set_option(gpu.OPT_JIT, 1)
-
-
 @pytest.mark.parametrize("name", ["C2", "C3"])
 @pytest.mark.parametrize("jit", [0, 1])
 def test_vertex_layouts_golden(gpu_poly, name, jit):
