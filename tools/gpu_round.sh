@@ -4,7 +4,8 @@
 # passes and the PMC sets (instruction mix, stalls, occupancy); then the driver's exact bench
 # command, the long C3 line and the C5 frame.  Every GPU step has its own time limit; the first
 # failure ends the script.
-# Usage (from the repo root, on the box): bash tools/gpu_round.sh TAG [notests] [nogui]
+# Usage (from the repo root, on the box): bash tools/gpu_round.sh TAG [notests] [nogui] [JITS]
+# (JITS: the tiers to profile, default "2 1"; e.g. "1" for the structure tier alone)
 # Only gpurun_out/ comes back from the box: afterwards, here, run
 #   bash tools/gpu_round.sh TAG --collect
 # to copy the summaries into profiles/ (baked tier: TAG_{kernel_stats.csv,traffic,pmc}.json;
@@ -34,7 +35,7 @@ if [ "$2" != "notests" ]; then
 fi
 # the driver's command with the kernels of one tier pinned (--jit J), no CPU leg / extras
 DRV="python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-extras"
-for J in 2 1; do
+for J in ${4:-2 1}; do
   D=$OUT/j$J
   mkdir -p $D
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/kt -o run -- $DRV --jit $J > $D/kt.log 2>&1 || { tail -20 $D/kt.log; exit 1; }
