@@ -1010,6 +1010,8 @@ void psgpu_destroy(psgpu_ctx* c) {
     if (c->hostStage) (void)hipHostFree(c->hostStage);
     for (int i = 0; i <= kNumKernels; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    for (hipEvent_t e : c->exportEv)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1433,23 +1435,40 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
     unsigned char* h = c->hostStage;
     hipStream_t s = c->stream;
     const size_t N = S.N, V = S.V, T = S.T;
+    for (hipEvent_t& e : c->exportEv)
+        if (!e) PSGPU_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (N) {
         if (mesh) PSGPU_CHECK(hipMemcpyAsync(h + S.oOffs, c->offs, (N + 1) * 8, hipMemcpyDeviceToHost, s));
         PSGPU_CHECK(hipMemcpyAsync(h + S.oPass, c->passed, N, hipMemcpyDeviceToHost, s));
         if (stats) PSGPU_CHECK(hipMemcpyAsync(h + S.oCnt, c->counts, N * 8, hipMemcpyDeviceToHost, s));
     }
-    if (V) {
-        PSGPU_CHECK(hipMemcpyAsync(h + S.oPos, c->pos, V * 12, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipMemcpyAsync(h + S.oNrm, c->nrm, V * 12, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipMemcpyAsync(h + S.oCol, c->col, V * 12, hipMemcpyDeviceToHost, s));
+    PSGPU_CHECK(hipEventRecord(c->exportEv[0], s));
+    // the mesh in pieces of equal vertex / triangle index ranges (4 for a mesh over 4 MB: the
+    // host scatter of one piece overlaps the PCIe copy of the next; 1 below that)
+    S.pieces = (V + T) * 12 > (4u << 20) ? 4 : 1;
+    for (int k = 0; k <= S.pieces; ++k) {
+        S.vPiece[k] = V * (size_t)k / (size_t)S.pieces;
+        S.tPiece[k] = T * (size_t)k / (size_t)S.pieces;
     }
-    if (T) PSGPU_CHECK(hipMemcpyAsync(h + S.oTris, c->tris, T * 12, hipMemcpyDeviceToHost, s));
+    for (int k = 0; k < S.pieces; ++k) {
+        const size_t v0 = S.vPiece[k], nv = S.vPiece[k + 1] - v0, t0 = S.tPiece[k], nt = S.tPiece[k + 1] - t0;
+        if (nv) {
+            PSGPU_CHECK(hipMemcpyAsync(h + S.oPos + v0 * 12, c->pos + v0 * 3, nv * 12, hipMemcpyDeviceToHost, s));
+            PSGPU_CHECK(hipMemcpyAsync(h + S.oNrm + v0 * 12, c->nrm + v0 * 3, nv * 12, hipMemcpyDeviceToHost, s));
+            PSGPU_CHECK(hipMemcpyAsync(h + S.oCol + v0 * 12, c->col + v0 * 3, nv * 12, hipMemcpyDeviceToHost, s));
+        }
+        if (nt) PSGPU_CHECK(hipMemcpyAsync(h + S.oTris + t0 * 12, c->tris + t0 * 3, nt * 12, hipMemcpyDeviceToHost, s));
+        PSGPU_CHECK(hipEventRecord(c->exportEv[k + 1], s));
+    }
     return PSGPU_RET_SUCCESS;
 }
 
 int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats) {
-    PSGPU_CHECK(hipStreamSynchronize(c->stream));
-    if (c->debug & (1 << 22)) return PSGPU_RET_SUCCESS;  // profiling: the copies without the scatter
+    PSGPU_CHECK(hipEventSynchronize(c->exportEv[0]));  // offsets, S1 flags, counts
+    if (c->debug & (1 << 22)) {  // profiling: the copies without the scatter
+        PSGPU_CHECK(hipStreamSynchronize(c->stream));
+        return PSGPU_RET_SUCCESS;
+    }
     const unsigned char* h = c->hostStage;
     const size_t N = S.N, V = S.V, T = S.T;
     const uint64_t* off = reinterpret_cast<const uint64_t*>(h + S.oOffs);
@@ -1462,7 +1481,21 @@ int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* 
         const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
         // the scatter is bound by the write-allocates of the sparse PolyMPUs layout (21.5 KB per
         // MPU): several host threads, as the reference's TBB bodies fill it
-        auto scatter = [&](uint32_t lb, uint32_t le) {
+        // MPUs [lb, le) need the mesh pieces up to the one holding their last vertex and triangle
+        auto wait_pieces = [&](uint32_t le, int* have) -> bool {
+            const size_t vEnd = (uint32_t)off[le], tEnd = (uint32_t)(off[le] >> 32);
+            int k = *have;
+            while (k < S.pieces && (S.vPiece[k] < vEnd || S.tPiece[k] < tEnd)) ++k;
+            for (; *have < k; ++*have)
+                if (hipEventSynchronize(c->exportEv[*have + 1]) != hipSuccess) return false;
+            return true;
+        };
+        std::atomic<bool> copyFailed{false};
+        auto scatter = [&](uint32_t lb, uint32_t le, int* have) {
+        if (!wait_pieces(le, have)) {
+            copyFailed = true;
+            return;
+        }
         for (uint32_t l = lb; l < le; ++l) {  // Polygonize :360-371
             const uint32_t m = c->mpuBegin + l;
             const uint32_t k = m % c->dims[2], j = (m / c->dims[2]) % c->dims[1], i = m / (c->dims[2] * c->dims[1]);
@@ -1481,15 +1514,19 @@ int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* 
             for (uint32_t t = 0; t < nt * 3; ++t) M.triangles[t] = (uint16_t)(tris[(size_t)t0 * 3 + t] - v0);
         }
         };
-        const size_t bytes = (V + T) * 12;  // ~1 thread per 256 KB of mesh, at most 8
-        const uint32_t nth = (uint32_t)std::min<size_t>({8, std::max(1u, std::thread::hardware_concurrency()),
+        const size_t bytes = (V + T) * 12;  // ~1 thread per 256 KB of mesh, at most 16
+        const uint32_t nth = (uint32_t)std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()),
                                                         1 + bytes / (256 << 10)});
         if (nth <= 1) {
-            scatter(0, (uint32_t)N);
+            int have = 0;
+            scatter(0, (uint32_t)N, &have);
         } else {
-            // chunks of 128 MPUs dealt round robin (the surface lies in a few slabs of the range)
+            // chunks of 128 MPUs dealt round robin (the surface lies in a few slabs of the range),
+            // each thread in ascending order, so the pieces are waited for in the order they come
             auto strided = [&](uint32_t k) {
-                for (uint32_t b = k * 128u; b < N; b += nth * 128u) scatter(b, std::min<uint32_t>((uint32_t)N, b + 128u));
+                int have = 0;
+                for (uint32_t b = k * 128u; b < N; b += nth * 128u)
+                    scatter(b, std::min<uint32_t>((uint32_t)N, b + 128u), &have);
             };
             std::vector<std::thread> th;
             for (uint32_t k = 1; k < nth; ++k) {
@@ -1502,7 +1539,9 @@ int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* 
             strided(0);
             for (std::thread& t : th) t.join();
         }
+        if (copyFailed) return PSGPU_RET_DEVICE_ERROR;
     }
+    PSGPU_CHECK(hipStreamSynchronize(c->stream));  // every piece in (stats only: the mesh copies too)
     if (stats && S.stats) {
         const uint64_t* cnt = reinterpret_cast<const uint64_t*>(h + S.oCnt);
         memset(stats, 0, sizeof(PsMpuStats) * N);

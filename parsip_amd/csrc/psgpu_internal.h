@@ -110,6 +110,7 @@ struct psgpu_ctx {
     DevCounters* hostCtrDev = nullptr;  // its device address
     unsigned char* hostStage = nullptr;  // pinned staging for the blocking PolyMPUs export
     size_t hostStageCap = 0;
+    hipEvent_t exportEv[5] = {};         // the export's copies: metadata, then up to 4 mesh pieces
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
     uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
     hipEvent_t ev[kNumKernels + 1] = {};
@@ -140,6 +141,11 @@ struct ExportStage {
     bool mesh = false, stats = false;
     size_t V = 0, T = 0, N = 0;
     size_t oOffs = 0, oPos = 0, oNrm = 0, oCol = 0, oTris = 0, oPass = 0, oCnt = 0;
+    // the mesh arrays come in `pieces` vertex / triangle index ranges [vPiece[k], vPiece[k+1]),
+    // each followed by exportEv[k + 1], so the scatter starts on the first piece while the
+    // others are still on PCIe
+    int pieces = 0;
+    size_t vPiece[5] = {}, tPiece[5] = {};
 };
 int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st);
 int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats);

@@ -14,7 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from parsip_amd import gpu, synth  # noqa: E402
 
 OPT = {"jit": gpu.OPT_JIT, "cull": gpu.OPT_CULLING, "debug": gpu.OPT_DEBUG, "graph": gpu.OPT_GRAPH, "vb": gpu.OPT_VERTEX_BLOCKS_PER_CU,
-       "fb": gpu.OPT_FINISH_BLOCKS_PER_CU, "bound": gpu.OPT_BOUND}
+       "fb": gpu.OPT_FINISH_BLOCKS_PER_CU, "bound": gpu.OPT_BOUND, "fq": gpu.OPT_FINISH_QUAD,
+       "vw": gpu.OPT_VERTEX_WIDE, "split": gpu.OPT_TREE_SPLIT}
 
 
 def main():
