@@ -454,22 +454,28 @@ int psgpu_group_export_polympus(psgpu_group* g, PsMPU* mpus, uint32_t capacity, 
     if (T.ctMPUs > capacity) return PSGPU_RET_MPU_OVERFLOW;
     if (T.firstOverflowMPU >= 0) return PSGPU_RET_MPU_VT_OVERFLOW;
     if (!mpus) return PSGPU_RET_PARAM_ERROR;
-    // every part's copies first (each on its own stream), then the scatters in range order:
-    // the later parts' downloads overlap the earlier parts' scatter
+    // every part's packing first (each on its own stream)
     std::vector<ExportStage> st(g->parts.size());
     for (size_t p = 0; p < g->parts.size(); ++p) {
         rc = set_device(g->parts[p]);
         if (rc == PSGPU_RET_SUCCESS) rc = export_stage(g->parts[p], true, false, &st[p]);
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
+    // then one pass of the first part's scatter threads over every part, in range order per
+    // thread: the parts' packing kernels share the link, the threads follow them
+    std::vector<ScatterJob> jobs(g->parts.size());
     uint32_t at = 0;
     for (size_t p = 0; p < g->parts.size(); ++p) {
-        rc = set_device(g->parts[p]);
-        if (rc == PSGPU_RET_SUCCESS) rc = export_scatter(g->parts[p], st[p], mpus + at, nullptr);
+        rc = jobs[p].prepare(g->parts[p], st[p], mpus + at);
         if (rc != PSGPU_RET_SUCCESS) return rc;
         at += g->parts[p]->mpuCount;
     }
-    return PSGPU_RET_SUCCESS;
+    rc = scatter_jobs(g->parts[0], jobs.data(), jobs.size());
+    for (size_t p = 0; p < g->parts.size() && rc == PSGPU_RET_SUCCESS; ++p) {
+        rc = set_device(g->parts[p]);
+        if (rc == PSGPU_RET_SUCCESS) rc = jobs[p].finish(nullptr);
+    }
+    return rc;
 }
 
 int psgpu_group_polygonize_mpus(psgpu_group* g, float cellsize, const PsSoaBlobPrims* prims,

@@ -1416,136 +1416,161 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
     S.T = mesh ? I.ctTriangles : 0;
     S.N = c->mpuCount;
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t N = S.N, V = S.V, T = S.T;
     S.oOffs = 0;
-    S.oPos = up(S.oOffs + (S.N + 1) * 8);
-    S.oNrm = up(S.oPos + S.V * 12);
-    S.oCol = up(S.oNrm + S.V * 12);
-    S.oTris = up(S.oCol + S.V * 12);
-    S.oPass = up(S.oTris + S.T * 12);
-    S.oCnt = up(S.oPass + S.N);
-    const size_t total = up(S.oCnt + (stats ? S.N * 8 : 0));
+    S.oPass = up((N + 1) * 8);
+    S.oCnt = up(S.oPass + N);
+    S.oMesh = up(S.oCnt + (stats ? N * 8 : 0));
+    // the packed mesh: pack_words per piece; bounded by 4 extra words per piece
+    S.meshBytes = mesh ? 4 * (pack_words(V, T) + 4 * kExportPieces) : 0;
+    S.oFlags = up(S.oMesh + S.meshBytes);
+    const size_t total = up(S.oFlags + 4 * (size_t)kExportPieces * kExportPackBlocksMax);
     if (total > c->hostStageCap) {
         if (c->hostStage) (void)hipHostFree(c->hostStage);
         c->hostStage = nullptr;
         c->hostStageCap = 0;
         const size_t cap = total + total / 4;
-        PSGPU_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c->hostStage), cap, hipHostMallocDefault));
+        // coherent: the export kernels write it directly over PCIe
+        PSGPU_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c->hostStage), cap,
+                                  hipHostMallocMapped | hipHostMallocCoherent));
         c->hostStageCap = cap;
+        memset(c->hostStage, 0, cap);  // no stale flag can equal an epoch
     }
+    if (++c->exportEpoch == 0) {  // wrapped: clear every old flag
+        memset(c->hostStage, 0, c->hostStageCap);
+        c->exportEpoch = 1;
+    }
+    S.epoch = c->exportEpoch;
     unsigned char* h = c->hostStage;
     hipStream_t s = c->stream;
-    const size_t N = S.N, V = S.V, T = S.T;
     for (hipEvent_t& e : c->exportEv)
         if (!e) PSGPU_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    unsigned char* hd = nullptr;  // the staging as the device addresses it
+    PSGPU_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hd), h, 0));
     if (N) {
-        if (mesh) PSGPU_CHECK(hipMemcpyAsync(h + S.oOffs, c->offs, (N + 1) * 8, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipMemcpyAsync(h + S.oPass, c->passed, N, hipMemcpyDeviceToHost, s));
-        if (stats) PSGPU_CHECK(hipMemcpyAsync(h + S.oCnt, c->counts, N * 8, hipMemcpyDeviceToHost, s));
+        MetaSrc ms{mesh ? c->offs : nullptr, c->passed, stats ? c->counts : nullptr, (uint32_t)N,
+                   S.oOffs, S.oPass, S.oCnt};
+        PSGPU_CHECK(launch_export_meta(ms, hd, s));
     }
     PSGPU_CHECK(hipEventRecord(c->exportEv[0], s));
-    // the mesh in pieces of equal vertex / triangle index ranges (4 for a mesh over 4 MB: the
-    // host scatter of one piece overlaps the PCIe copy of the next; 1 below that)
-    S.pieces = (V + T) * 12 > (4u << 20) ? 4 : 1;
-    for (int k = 0; k <= S.pieces; ++k) {
-        S.vPiece[k] = V * (size_t)k / (size_t)S.pieces;
-        S.tPiece[k] = T * (size_t)k / (size_t)S.pieces;
+    // the mesh packed piece by piece (MPU ranges of about 1 MB of mesh, at most 16) into one
+    // contiguous region by one kernel writing it over PCIe; the host scatter of one piece
+    // overlaps the transfer of the next
+    static const size_t pieceBytes = getenv("PSGPU_EXPORT_PIECE_KB") ? (size_t)atoi(getenv("PSGPU_EXPORT_PIECE_KB")) << 10 : kExportPieceBytes;  // A/B
+    static const uint32_t packBlocks = getenv("PSGPU_PACK_BLOCKS") ? (uint32_t)atoi(getenv("PSGPU_PACK_BLOCKS")) : 256;  // A/B
+    S.packBlocks = std::min(packBlocks, kExportPackBlocksMax);
+    S.pieces = (int)std::min<size_t>({(size_t)kExportPieces, std::max<size_t>(N, 1),
+                                      1 + 4 * pack_words(V, T) / pieceBytes});
+    if (S.meshBytes && N) {
+        PackSrc src{c->offs, c->pos, c->nrm, c->col, c->tris, (uint32_t)N, (uint32_t)S.pieces,
+                    reinterpret_cast<uint32_t*>(hd + S.oFlags), S.epoch, S.packBlocks};
+        PSGPU_CHECK(launch_export_pack(src, reinterpret_cast<uint32_t*>(hd + S.oMesh), s));
     }
-    for (int k = 0; k < S.pieces; ++k) {
-        const size_t v0 = S.vPiece[k], nv = S.vPiece[k + 1] - v0, t0 = S.tPiece[k], nt = S.tPiece[k + 1] - t0;
-        if (nv) {
-            PSGPU_CHECK(hipMemcpyAsync(h + S.oPos + v0 * 12, c->pos + v0 * 3, nv * 12, hipMemcpyDeviceToHost, s));
-            PSGPU_CHECK(hipMemcpyAsync(h + S.oNrm + v0 * 12, c->nrm + v0 * 3, nv * 12, hipMemcpyDeviceToHost, s));
-            PSGPU_CHECK(hipMemcpyAsync(h + S.oCol + v0 * 12, c->col + v0 * 3, nv * 12, hipMemcpyDeviceToHost, s));
-        }
-        if (nt) PSGPU_CHECK(hipMemcpyAsync(h + S.oTris + t0 * 12, c->tris + t0 * 3, nt * 12, hipMemcpyDeviceToHost, s));
-        PSGPU_CHECK(hipEventRecord(c->exportEv[k + 1], s));
+    PSGPU_CHECK(hipEventRecord(c->exportEv[1], s));
+    return PSGPU_RET_SUCCESS;
+}
+
+int ScatterJob::prepare(psgpu_ctx* ctx, const ExportStage& st, PsMPU* out) {
+    c = ctx;
+    S = &st;
+    mpus = out;
+    PSGPU_CHECK(hipEventSynchronize(c->exportEv[0]));  // offsets, S1 flags, counts
+    const unsigned char* h = c->hostStage;
+    off = reinterpret_cast<const uint64_t*>(h + st.oOffs);
+    passed = h + st.oPass;
+    mesh = h + st.oMesh;
+    flags = reinterpret_cast<const uint32_t*>(h + st.oFlags);
+    side = c->cs * (float)PSGPU_CELLS_PER_MPU;
+    active = out && st.mesh && !(c->debug & (1 << 22));  // bit 22: the transfers without the scatter
+    if (!active) return PSGPU_RET_SUCCESS;
+    // the pieces' MPU ranges and their places in the packed mesh (as k_export_pack laid them out)
+    const size_t N = st.N;
+    size_t base = 0;
+    for (int k = 0; k <= st.pieces; ++k) pm[k] = (uint32_t)((uint64_t)N * (uint64_t)k / (uint64_t)st.pieces);
+    for (int k = 0; k < st.pieces; ++k) {
+        pv0[k] = (uint32_t)off[pm[k]];
+        pt0[k] = (uint32_t)(off[pm[k]] >> 32);
+        pnv[k] = (uint32_t)off[pm[k + 1]] - pv0[k];
+        pbase[k] = base;
+        base += 4 * pack_words(pnv[k], (uint32_t)(off[pm[k + 1]] >> 32) - pt0[k]);
     }
     return PSGPU_RET_SUCCESS;
 }
 
-int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats) {
-    PSGPU_CHECK(hipEventSynchronize(c->exportEv[0]));  // offsets, S1 flags, counts
-    if (c->debug & (1 << 22)) {  // profiling: the copies without the scatter
-        PSGPU_CHECK(hipStreamSynchronize(c->stream));
-        return PSGPU_RET_SUCCESS;
+// piece k is in when every block of k_export_pack has raised its flag for it; the kernel's
+// event ends the wait should it fail
+bool ScatterJob::wait_piece(int k) const {
+    const uint32_t* f = flags + (size_t)k * S->packBlocks;
+    uint32_t b = 0;
+    for (uint32_t spin = 1;; ++spin) {
+        while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
+        if (b == S->packBlocks) return true;
+        if ((spin & 255) == 0) {
+            const hipError_t e = hipEventQuery(c->exportEv[1]);
+            if (e == hipSuccess) {  // the kernel is done: every flag must be up now
+                while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
+                return b == S->packBlocks;
+            }
+            if (e != hipErrorNotReady) return false;
+        }
+        std::this_thread::yield();
     }
-    const unsigned char* h = c->hostStage;
-    const size_t N = S.N, V = S.V, T = S.T;
-    const uint64_t* off = reinterpret_cast<const uint64_t*>(h + S.oOffs);
-    const float* pos = reinterpret_cast<const float*>(h + S.oPos);
-    const float* nrm = reinterpret_cast<const float*>(h + S.oNrm);
-    const float* col = reinterpret_cast<const float*>(h + S.oCol);
-    const uint32_t* tris = reinterpret_cast<const uint32_t*>(h + S.oTris);
-    const uint8_t* passed = h + S.oPass;
-    if (mpus && S.mesh) {
-        const float side = c->cs * (float)PSGPU_CELLS_PER_MPU;
-        // the scatter is bound by the write-allocates of the sparse PolyMPUs layout (21.5 KB per
-        // MPU): several host threads, as the reference's TBB bodies fill it
-        // MPUs [lb, le) need the mesh pieces up to the one holding their last vertex and triangle
-        auto wait_pieces = [&](uint32_t le, int* have) -> bool {
-            const size_t vEnd = (uint32_t)off[le], tEnd = (uint32_t)(off[le] >> 32);
-            int k = *have;
-            while (k < S.pieces && (S.vPiece[k] < vEnd || S.tPiece[k] < tEnd)) ++k;
-            for (; *have < k; ++*have)
-                if (hipEventSynchronize(c->exportEv[*have + 1]) != hipSuccess) return false;
-            return true;
-        };
-        std::atomic<bool> copyFailed{false};
-        auto scatter = [&](uint32_t lb, uint32_t le, int* have) {
-        if (!wait_pieces(le, have)) {
-            copyFailed = true;
+}
+
+// MPUs [lb, le) into PolyMPUs (Polygonize :360-371); `have` = the pieces this thread has seen in
+bool ScatterJob::range(uint32_t lb, uint32_t le, int* have) const {
+    int k = 0;
+    while (k + 1 < S->pieces && lb >= pm[k + 1]) ++k;
+    for (uint32_t l = lb; l < le; ++l) {
+        while (k + 1 < S->pieces && l >= pm[k + 1]) ++k;
+        const uint32_t v0 = (uint32_t)off[l], nv = (uint32_t)off[l + 1] - v0;
+        const uint32_t t0 = (uint32_t)(off[l] >> 32), nt = (uint32_t)(off[l + 1] >> 32) - t0;
+        const unsigned char* P = mesh + pbase[k];
+        const float* pos = reinterpret_cast<const float*>(P) + 3 * (v0 - pv0[k]);
+        const float* nrm = reinterpret_cast<const float*>(P + pnv[k] * 12) + 3 * (v0 - pv0[k]);
+        const float* col = reinterpret_cast<const float*>(P + pnv[k] * 24) + 3 * (v0 - pv0[k]);
+        const uint16_t* tri = reinterpret_cast<const uint16_t*>(P + pnv[k] * 36) + 3 * (t0 - pt0[k]);
+        while (*have <= k) {  // this MPU's piece written (the pieces come in order)
+            if (!wait_piece(*have)) return false;
+            ++*have;
+        }
+        const uint32_t m = c->mpuBegin + l;
+        const uint32_t kk = m % c->dims[2], j = (m / c->dims[2]) % c->dims[1], i = m / (c->dims[2] * c->dims[1]);
+        PsMPU& M = mpus[l];
+        M.bboxLo.x = c->primsHost.bboxLo.x + (float)i * side;
+        M.bboxLo.y = c->primsHost.bboxLo.y + (float)j * side;
+        M.bboxLo.z = c->primsHost.bboxLo.z + (float)kk * side;
+        M.ctFieldEvals = passed[l] ? 128 : 0;
+        M.ctVertices = (uint16_t)nv;
+        M.ctTriangles = (uint16_t)nt;
+        memcpy(M.vPos, pos, (size_t)nv * 12);
+        memcpy(M.vNorm, nrm, (size_t)nv * 12);
+        memcpy(M.vColor, col, (size_t)nv * 12);
+        memcpy(M.triangles, tri, (size_t)nt * 6);
+    }
+    return true;
+}
+
+// thread k of nth: chunks of 128 MPUs dealt round robin (the surface lies in a few slabs of
+// the range), in ascending order, so the pieces are waited for in the order they come
+void ScatterJob::task(unsigned k, unsigned nth) {
+    if (!active) return;
+    int have = 0;
+    const uint32_t N = (uint32_t)S->N;
+    for (uint32_t b = k * 128u; b < N; b += nth * 128u)
+        if (!range(b, std::min<uint32_t>(N, b + 128u), &have)) {
+            failed = true;
             return;
         }
-        for (uint32_t l = lb; l < le; ++l) {  // Polygonize :360-371
-            const uint32_t m = c->mpuBegin + l;
-            const uint32_t k = m % c->dims[2], j = (m / c->dims[2]) % c->dims[1], i = m / (c->dims[2] * c->dims[1]);
-            PsMPU& M = mpus[l];
-            M.bboxLo.x = c->primsHost.bboxLo.x + (float)i * side;
-            M.bboxLo.y = c->primsHost.bboxLo.y + (float)j * side;
-            M.bboxLo.z = c->primsHost.bboxLo.z + (float)k * side;
-            M.ctFieldEvals = passed[l] ? 128 : 0;
-            const uint32_t v0 = (uint32_t)off[l], nv = (uint32_t)off[l + 1] - v0;
-            const uint32_t t0 = (uint32_t)(off[l] >> 32), nt = (uint32_t)(off[l + 1] >> 32) - t0;
-            M.ctVertices = (uint16_t)nv;
-            M.ctTriangles = (uint16_t)nt;
-            memcpy(M.vPos, pos + (size_t)v0 * 3, (size_t)nv * 12);
-            memcpy(M.vNorm, nrm + (size_t)v0 * 3, (size_t)nv * 12);
-            memcpy(M.vColor, col + (size_t)v0 * 3, (size_t)nv * 12);
-            for (uint32_t t = 0; t < nt * 3; ++t) M.triangles[t] = (uint16_t)(tris[(size_t)t0 * 3 + t] - v0);
-        }
-        };
-        const size_t bytes = (V + T) * 12;  // ~1 thread per 256 KB of mesh, at most 16
-        const uint32_t nth = (uint32_t)std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()),
-                                                        1 + bytes / (256 << 10)});
-        if (nth <= 1) {
-            int have = 0;
-            scatter(0, (uint32_t)N, &have);
-        } else {
-            // chunks of 128 MPUs dealt round robin (the surface lies in a few slabs of the range),
-            // each thread in ascending order, so the pieces are waited for in the order they come
-            auto strided = [&](uint32_t k) {
-                int have = 0;
-                for (uint32_t b = k * 128u; b < N; b += nth * 128u)
-                    scatter(b, std::min<uint32_t>((uint32_t)N, b + 128u), &have);
-            };
-            std::vector<std::thread> th;
-            for (uint32_t k = 1; k < nth; ++k) {
-                try {
-                    th.emplace_back(strided, k);
-                } catch (...) {  // no thread to be had: this caller does the chunks itself
-                    strided(k);
-                }
-            }
-            strided(0);
-            for (std::thread& t : th) t.join();
-        }
-        if (copyFailed) return PSGPU_RET_DEVICE_ERROR;
-    }
-    PSGPU_CHECK(hipStreamSynchronize(c->stream));  // every piece in (stats only: the mesh copies too)
-    if (stats && S.stats) {
-        const uint64_t* cnt = reinterpret_cast<const uint64_t*>(h + S.oCnt);
-        memset(stats, 0, sizeof(PsMpuStats) * N);
-        for (uint32_t l = 0; l < N; ++l) {
+}
+
+int ScatterJob::finish(PsMpuStats* stats) {
+    if (failed) return PSGPU_RET_DEVICE_ERROR;
+    PSGPU_CHECK(hipStreamSynchronize(c->stream));  // the packing kernel done
+    if (stats && S->stats) {
+        const uint64_t* cnt = reinterpret_cast<const uint64_t*>(c->hostStage + S->oCnt);
+        memset(stats, 0, sizeof(PsMpuStats) * S->N);
+        for (uint32_t l = 0; l < S->N; ++l) {
             PsMpuStats& st = stats[l];
             if (passed[l]) {
                 st.passedPrecheck = 1;
@@ -1556,6 +1581,41 @@ int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* 
         }
     }
     return PSGPU_RET_SUCCESS;
+}
+
+// The scatter is bound by the write-allocates of the sparse PolyMPUs layout (21.5 KB per MPU):
+// several host threads, as the reference's TBB bodies fill it -- about one per 256 KB of mesh,
+// at most 16, kept in c's pool.  Runs jobs[0..n) in one pass: every thread takes its chunks of
+// each job in turn.
+int scatter_jobs(psgpu_ctx* c, ScatterJob* jobs, size_t n) {
+    size_t bytes = 0;
+    for (size_t j = 0; j < n; ++j) bytes += jobs[j].active ? jobs[j].S->meshBytes : 0;
+    static const size_t maxTh = getenv("PSGPU_SCATTER_THREADS") ? (size_t)atoi(getenv("PSGPU_SCATTER_THREADS")) : 16;  // A/B
+    const unsigned nth = (unsigned)std::min<size_t>({maxTh, std::max(1u, std::thread::hardware_concurrency()),
+                                                    1 + bytes / (256 << 10)});
+    std::function<void(unsigned)> task = [&](unsigned k) {
+        for (size_t j = 0; j < n; ++j) jobs[j].task(k, nth);
+    };
+    if (nth > 1 && (!c->scatterPool || c->scatterPool->workers() + 1 < nth)) {
+        c->scatterPool.reset();
+        try {
+            c->scatterPool.reset(new ScatterPool(nth - 1));
+        } catch (...) {  // no threads to be had: this caller scatters alone
+            c->scatterPool.reset();
+        }
+    }
+    if (nth > 1 && c->scatterPool) c->scatterPool->run(nth, task);
+    else
+        for (unsigned k = 0; k < nth; ++k) task(k);
+    return PSGPU_RET_SUCCESS;
+}
+
+int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats) {
+    ScatterJob job;
+    int rc = job.prepare(c, S, mpus);
+    if (rc == PSGPU_RET_SUCCESS) rc = scatter_jobs(c, &job, 1);
+    if (rc == PSGPU_RET_SUCCESS) rc = job.finish(stats);
+    return rc;
 }
 }  // namespace psgpu
 

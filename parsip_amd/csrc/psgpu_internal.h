@@ -4,8 +4,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/parsip_gpu.h"
 #include "psgpu_jit.h"
@@ -13,6 +20,86 @@
 
 namespace psgpu {
 constexpr int kNumKernels = 4;
+}  // namespace psgpu
+
+namespace psgpu {
+// Host threads kept for the blocking export's scatter (psgpu_host.cpp export_scatter): spawning
+// them per call cost more than the scatter of a small mesh.  run(n, f) calls f(0 .. n-1) over
+// the workers and the caller and returns when every call has returned.  A task is claimed by a
+// compare-exchange on one word holding (job, count, next), so a worker still leaving the last
+// job can never take a task of the next one.
+constexpr int kExportPieces = 16;  // at most, in the blocking export (psgpu_host.cpp export_stage)
+constexpr size_t kExportPieceBytes = 1u << 20;  // its target piece size
+
+class ScatterPool {
+public:
+    explicit ScatterPool(unsigned workers) {
+        for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this] { work(); });
+    }
+    ~ScatterPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    unsigned workers() const { return (unsigned)th_.size(); }
+    void run(unsigned n, const std::function<void(unsigned)>& f) {
+        if (!n) return;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            f_ = &f;
+            left_.store(n, std::memory_order_relaxed);
+            ++gen_;
+            state_.store(((uint64_t)gen_ << 32) | ((uint64_t)n << 16), std::memory_order_release);
+        }
+        cv_.notify_all();
+        drain(gen_);
+        std::unique_lock<std::mutex> l(mu_);
+        done_.wait(l, [&] { return left_.load(std::memory_order_acquire) == 0; });
+    }
+
+private:
+    void drain(uint32_t gen) {
+        uint64_t v = state_.load(std::memory_order_acquire);
+        for (;;) {
+            if ((uint32_t)(v >> 32) != gen || (v & 0xffffu) >= ((v >> 16) & 0xffffu)) return;
+            if (!state_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
+            (*f_)((unsigned)(v & 0xffffu));
+            if (left_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> g(mu_);
+                done_.notify_all();
+            }
+            v = state_.load(std::memory_order_acquire);
+        }
+    }
+    void work() {
+        uint32_t seen = 0;
+        for (;;) {
+            // a short spin for the next job (back-to-back calls), then sleep
+            const auto t0 = std::chrono::steady_clock::now();
+            while ((uint32_t)(state_.load(std::memory_order_acquire) >> 32) == seen &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+                std::this_thread::yield();
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [&] { return stop_ || (uint32_t)(state_.load(std::memory_order_acquire) >> 32) != seen; });
+                if (stop_) return;
+            }
+            seen = (uint32_t)(state_.load(std::memory_order_acquire) >> 32);
+            drain(seen);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* f_ = nullptr;
+    std::atomic<uint64_t> state_{0};  // job << 32 | count << 16 | next
+    std::atomic<uint32_t> left_{0};
+    uint32_t gen_ = 0;
+    bool stop_ = false;
+};
 }  // namespace psgpu
 
 struct psgpu_ctx {
@@ -110,7 +197,9 @@ struct psgpu_ctx {
     DevCounters* hostCtrDev = nullptr;  // its device address
     unsigned char* hostStage = nullptr;  // pinned staging for the blocking PolyMPUs export
     size_t hostStageCap = 0;
-    hipEvent_t exportEv[5] = {};         // the export's copies: metadata, then up to 4 mesh pieces
+    hipEvent_t exportEv[2] = {};         // the export's metadata, then its packing kernel
+    uint32_t exportEpoch = 0;            // the blocking export's flag value (k_export_pack), never 0
+    std::unique_ptr<psgpu::ScatterPool> scatterPool;  // the export's scatter threads, made on first use
     uint32_t vcap = 1u << 20, tcap = 1u << 21;               // compact mesh capacity
     uint32_t vShardCap = 1u << 15, tShardCap = 1u << 16;      // work-queue capacity per shard
     hipEvent_t ev[kNumKernels + 1] = {};
@@ -141,14 +230,38 @@ struct ExportStage {
     bool mesh = false, stats = false;
     size_t V = 0, T = 0, N = 0;
     size_t oOffs = 0, oPos = 0, oNrm = 0, oCol = 0, oTris = 0, oPass = 0, oCnt = 0;
-    // the mesh arrays come in `pieces` vertex / triangle index ranges [vPiece[k], vPiece[k+1]),
-    // each followed by exportEv[k + 1], so the scatter starts on the first piece while the
-    // others are still on PCIe
+    // the mesh, packed as `pieces` MPU ranges (pos | nrm | col | 16-bit triangle corners of
+    // each, psgpu_launch.h PackSrc) at oMesh, piece k complete when its packBlocks flags at
+    // oFlags + 4 k packBlocks equal epoch: the scatter of one piece overlaps the
+    // transfer of the next
     int pieces = 0;
-    size_t vPiece[5] = {}, tPiece[5] = {};
+    size_t oMesh = 0, meshBytes = 0, oFlags = 0;
+    uint32_t epoch = 0, packBlocks = 0;
 };
 int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st);
 int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats);
+// One staged export's scatter into PolyMPUs, split so that a group's parts go in one pass of
+// the thread pool (scatter_jobs): prepare (after the metadata), task per thread, finish.
+struct ScatterJob {
+    psgpu_ctx* c = nullptr;
+    const ExportStage* S = nullptr;
+    PsMPU* mpus = nullptr;
+    const uint64_t* off = nullptr;
+    const uint8_t* passed = nullptr;
+    const unsigned char* mesh = nullptr;
+    const uint32_t* flags = nullptr;
+    float side = 0.0f;
+    bool active = false;
+    std::atomic<bool> failed{false};
+    uint32_t pm[kExportPieces + 1] = {};
+    size_t pbase[kExportPieces] = {}, pv0[kExportPieces] = {}, pt0[kExportPieces] = {}, pnv[kExportPieces] = {};
+    int prepare(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus);
+    bool wait_piece(int k) const;
+    bool range(uint32_t lb, uint32_t le, int* have) const;
+    void task(unsigned k, unsigned nth);
+    int finish(PsMpuStats* stats);
+};
+int scatter_jobs(psgpu_ctx* c, ScatterJob* jobs, size_t n);
 }  // namespace psgpu
 
 #define PSGPU_CHECK(expr)                                           \

@@ -85,6 +85,60 @@ __global__ void __launch_bounds__(64) k_sum_totals(TotalsParts tp, uint32_t* __r
     out[i] = v;
 }
 
+// The blocking export's packing (psgpu_launch.h PackSrc), written straight into the pinned host
+// staging over PCIe -- no copy-engine transfers (each cost ~13 us of setup, r04) and one launch:
+// every block walks the pieces in order, writes its share of one, then raises its flag for it
+// (flags[piece * gridDim.x + block] = epoch, a system-scope release), so the host scatters
+// piece k while piece k + 1 is still on the link.
+__global__ void __launch_bounds__(256) k_export_pack(PackSrc src, uint32_t* __restrict__ dst) {
+    uint64_t base = 0;  // the piece's first word
+    for (uint32_t k = 0; k < src.pieces; ++k) {
+        const uint32_t m0 = (uint32_t)((uint64_t)src.n * k / src.pieces);
+        const uint32_t m1 = (uint32_t)((uint64_t)src.n * (k + 1) / src.pieces);
+        const uint64_t a = src.offs[m0], b = src.offs[m1];
+        const uint32_t v0 = (uint32_t)a, v1 = (uint32_t)b, t0 = (uint32_t)(a >> 32), t1 = (uint32_t)(b >> 32);
+        const uint64_t nv = 3ull * (v1 - v0);  // words per vertex array
+        const uint64_t ne = 3ull * (t1 - t0);  // triangle corners, two 16-bit local indices a word
+        const uint32_t* pos = reinterpret_cast<const uint32_t*>(src.pos) + 3ull * v0;
+        const uint32_t* nrm = reinterpret_cast<const uint32_t*>(src.nrm) + 3ull * v0;
+        const uint32_t* col = reinterpret_cast<const uint32_t*>(src.col) + 3ull * v0;
+        const uint32_t* tri = src.tris + 3ull * t0;
+        const uint64_t total = 3 * nv + (ne + 1) / 2;
+        // a corner's index relative to its MPU's first vertex (PolyMPUs' uint16 triangles,
+        // Polygonize :368): the MPU from a binary search of the piece's triangle offsets
+        auto local = [&](uint64_t e) -> uint32_t {
+            const uint32_t t = t0 + (uint32_t)(e / 3);
+            uint32_t lo = m0, hi = m1;  // offs_t[lo] <= t < offs_t[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((uint32_t)(src.offs[mid] >> 32) <= t) lo = mid;
+                else hi = mid;
+            }
+            return (tri[e] - (uint32_t)src.offs[lo]) & 0xffffu;
+        };
+        uint32_t* out = dst + base;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+            uint32_t w;
+            if (i < nv) w = pos[i];
+            else if (i < 2 * nv) w = nrm[i - nv];
+            else if (i < 3 * nv) w = col[i - 2 * nv];
+            else {
+                const uint64_t e = 2 * (i - 3 * nv);
+                w = local(e) | (e + 1 < ne ? local(e + 1) << 16 : 0u);
+            }
+            out[i] = w;
+        }
+        base += pack_words(v1 - v0, t1 - t0);
+        // every wave's stores acknowledged, then one system-scope release per block (its L2
+        // write-back covers the block's words) before the flag: one fence a block, not a wave
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(src.flags + (uint64_t)k * gridDim.x + blockIdx.x, src.epoch, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (psgpu_launch.h).
 size_t mpu_lds_bytes(uint32_t slots) { return kLdsWaveSlots + 4 * ((size_t)slots * 64 * 4); }
@@ -124,6 +178,29 @@ hipError_t launch_rebase(uint32_t* tris, uint64_t nTri, uint32_t vBase, uint64_t
     uint64_t blocks = (n + 1023) / 1024;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(k_rebase, dim3((uint32_t)blocks), dim3(256), 0, s, tris, nTri, vBase, offs, nOff, offBase);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_pack(const PackSrc& src, uint32_t* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_export_pack, dim3(src.blocks), dim3(256), 0, s, src, dst);
+    return hipGetLastError();
+}
+
+// The export's metadata (offsets, S1 flags, per-MPU counts) into the pinned host staging.
+__global__ void __launch_bounds__(256) k_export_meta(MetaSrc src, unsigned char* __restrict__ dst) {
+    const uint64_t nOff = src.offs ? 2ull * (src.n + 1) : 0, nCnt = src.counts ? 2ull * src.n : 0;
+    const uint32_t* offs = reinterpret_cast<const uint32_t*>(src.offs);
+    const uint32_t* cnt = reinterpret_cast<const uint32_t*>(src.counts);
+    uint32_t* dOff = reinterpret_cast<uint32_t*>(dst + src.oOffs);
+    uint32_t* dCnt = reinterpret_cast<uint32_t*>(dst + src.oCnt);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nOff; i += stride) dOff[i] = offs[i];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nCnt; i += stride) dCnt[i] = cnt[i];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < src.n; i += stride)
+        dst[src.oPass + i] = src.passed[i];
+}
+hipError_t launch_export_meta(const MetaSrc& src, unsigned char* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_export_meta, dim3(128), dim3(256), 0, s, src, dst);
     return hipGetLastError();
 }
 

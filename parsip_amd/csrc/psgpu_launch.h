@@ -25,5 +25,31 @@ struct TotalsParts {  // the k_finish totals (8 words) of up to 16 parts on one 
 hipError_t launch_sum_totals(const TotalsParts& tp, uint32_t* out, hipStream_t s);
 hipError_t launch_rebase(uint32_t* tris, uint64_t nTri, uint32_t vBase, uint64_t* offs, uint64_t nOff,
                          uint64_t offBase, hipStream_t s);
+// The compact mesh of `pieces` MPU ranges [N k / pieces, N (k+1) / pieces), packed piece by
+// piece as pos | nrm | col (float words) | triangle corners as 16-bit indices relative to their
+// MPU's first vertex, two a word (PolyMPUs' triangles): one contiguous buffer the blocking
+// export's staging receives piece by piece.  A piece of nv vertices, nt triangles takes
+// pack_words(nv, nt) words.
+inline __host__ __device__ uint64_t pack_words(uint64_t nv, uint64_t nt) {
+    return (9 * nv + (3 * nt + 1) / 2 + 3) & ~(uint64_t)3;  // padded to 16 bytes
+}
+struct PackSrc {
+    const uint64_t* offs;
+    const float *pos, *nrm, *col;
+    const uint32_t* tris;
+    uint32_t n, pieces;
+    uint32_t* flags;  // [pieces][blocks], set to epoch as each block finishes a piece
+    uint32_t epoch, blocks;
+};
+constexpr uint32_t kExportPackBlocksMax = 2048;
+hipError_t launch_export_pack(const PackSrc& src, uint32_t* dst, hipStream_t s);
+struct MetaSrc {  // offs / counts null when not exported
+    const uint64_t* offs;
+    const uint8_t* passed;
+    const uint64_t* counts;
+    uint32_t n;
+    size_t oOffs, oPass, oCnt;  // byte offsets in dst
+};
+hipError_t launch_export_meta(const MetaSrc& src, unsigned char* dst, hipStream_t s);
 
 }  // namespace psgpu
