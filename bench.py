@@ -628,6 +628,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):  # step k is one complete polygonization, on engine k mod E
         engines[k % neng].polygonize()
+    t_enq = time.perf_counter()
     results = [e.finish() for e in engines]
     grp.barrier()
     t1 = time.perf_counter()
@@ -863,7 +864,8 @@ def main():
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
                    "exchange": exchange, "culling": not args.no_cull, "tree_split": args.tree_split,
                    "kernels": kernels_label, "tiers": tiers_timed, "set_model_s": round(t_model, 4),
-                   "jit_ready_s": round(t_jit, 3)},
+                   "jit_ready_s": round(t_jit, 3),
+                   "host_enqueue_ms": round((t_enq - t0) * 1e3, 4)},
         "roofline": roof,
         "kernel_ms_per_launch": {k: round(v, 4) for k, v in kt.items()},
         "kernel_ms_per_launch_hipevent": {k: round(v, 4) for k, v in ev_ms.items()},

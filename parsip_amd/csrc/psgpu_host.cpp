@@ -1424,7 +1424,7 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
     // the packed mesh: pack_words per piece; bounded by 4 extra words per piece
     S.meshBytes = mesh ? 4 * (pack_words(V, T) + 4 * kExportPieces) : 0;
     S.oFlags = up(S.oMesh + S.meshBytes);
-    const size_t total = up(S.oFlags + 4 * (size_t)kExportPieces * kExportPackBlocksMax);
+    const size_t total = up(S.oFlags + 4 * (size_t)kExportPieces * kExportPackBlocks);
     if (total > c->hostStageCap) {
         if (c->hostStage) (void)hipHostFree(c->hostStage);
         c->hostStage = nullptr;
@@ -1457,8 +1457,9 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
     // contiguous region by one kernel writing it over PCIe; the host scatter of one piece
     // overlaps the transfer of the next
     static const size_t pieceBytes = getenv("PSGPU_EXPORT_PIECE_KB") ? (size_t)atoi(getenv("PSGPU_EXPORT_PIECE_KB")) << 10 : kExportPieceBytes;  // A/B
-    static const uint32_t packBlocks = getenv("PSGPU_PACK_BLOCKS") ? (uint32_t)atoi(getenv("PSGPU_PACK_BLOCKS")) : 256;  // A/B
-    S.packBlocks = std::min(packBlocks, kExportPackBlocksMax);
+    // 256 blocks: one wave per SIMD keeps the link busy; 1,024 or 2,048 were 1.8-4.5x slower,
+    // every block's per-piece release (an L2 write-back) adding up (r04)
+    S.packBlocks = kExportPackBlocks;
     S.pieces = (int)std::min<size_t>({(size_t)kExportPieces, std::max<size_t>(N, 1),
                                       1 + 4 * pack_words(V, T) / pieceBytes});
     if (S.meshBytes && N) {

@@ -41,7 +41,7 @@ struct PackSrc {
     uint32_t* flags;  // [pieces][blocks], set to epoch as each block finishes a piece
     uint32_t epoch, blocks;
 };
-constexpr uint32_t kExportPackBlocksMax = 2048;
+constexpr uint32_t kExportPackBlocks = 256;
 hipError_t launch_export_pack(const PackSrc& src, uint32_t* dst, hipStream_t s);
 struct MetaSrc {  // offs / counts null when not exported
     const uint64_t* offs;

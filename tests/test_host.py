@@ -192,3 +192,19 @@ def test_cpp_shim_compiles_and_runs(tmp_path):
                     f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_export_thread_pool(tmp_path):
+    """The blocking export's scatter threads (psgpu_pool.h): every task of every run exactly
+    once, run returns only after all, with the workers spinning or asleep."""
+    import shutil
+    import subprocess
+
+    gpp = shutil.which("g++")
+    if gpp is None:
+        pytest.skip("no g++")
+    exe = tmp_path / "pool_check"
+    subprocess.run([gpp, "-std=c++17", "-O2", "-Wall", "-pthread", "-I", os.path.join(ROOT, "parsip_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "cpp", "pool_check.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
