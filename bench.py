@@ -295,8 +295,8 @@ def blocking_contract(poly, config="C2", reps=10):
     """The reference's own blocking contract, PCIe-inclusive: Polygonize into the caller's
     PolyMPUs (PS_Polygonizer.h:386-391 as SimdPoly::run calls it, PS_HighPerformanceRender.cpp:
     373-376): model upload, polygonization, mesh download and the scatter into the sparse
-    21.5-KB-per-MPU PolyMPUs layout.  `poly` is the drop-in's engine: the default 2-part group
-    of psgpu::Polygonize / gpu.Polygonize (a gpu.Group) or one context (gpu.Polygonizer).  C3
+    21.5-KB-per-MPU PolyMPUs layout.  `poly` is one context (gpu.Polygonizer: what
+    psgpu::Polygonize / gpu.Polygonize run on) or a gpu.Group of parts of the device.  C3
     has 50,653 MPUs, past the reference's MAX_MPU_COUNT (24,000), so its PolyMPUs array is
     allocated with room for them (1.09 GB).  Median over `reps` calls after 2 warm-ups."""
     from parsip_amd import soa
@@ -313,8 +313,8 @@ def blocking_contract(poly, config="C2", reps=10):
         poly.polygonize_mpus(cs, model, out)
         t.append(time.perf_counter() - t0)
     med = float(np.median(t))
-    engine = (f"psgpu_group_polygonize_mpus over {poly.n} parts of one device (the drop-in's default)"
-              if isinstance(poly, gpu.Group) else "psgpu_polygonize_mpus on one context")
+    engine = (f"psgpu_group_polygonize_mpus over {poly.n} parts of one device"
+              if isinstance(poly, gpu.Group) else "psgpu_polygonize_mpus on one context (the drop-ins' default)")
     return {"config": f"{config}: {model.ct_prims}-prim BlobTree, {n}^3 cells, {ct} MPUs", "ms": round(med * 1e3, 3),
             "best_ms": round(min(t) * 1e3, 3), "mcells_per_s": round(n ** 3 / med / 1e6, 2), "engine": engine,
             "note": "end to end (SoA upload, the kernel chains, compact-mesh download over PCIe, host scatter into "
@@ -887,16 +887,19 @@ def main():
                                     "note": "one engine, one polygonization at a time, host-timed "
                                             "(enqueue + kernel chain + sync): a blocking caller's latency"}
         out["latency_ms_single_parts"] = latency_single_parts(device, model, cs, args.jit)
+        # the drop-ins' blocking contract (psgpu::Polygonize / gpu.Polygonize: one context), C2
+        # and the headline's C3; beside it C3 on a 2-part group of the device (shorter kernels,
+        # slower export: DESIGN.md §4 "Blocking")
+        out["blocking_polygonize_mpus"] = blocking_contract(poly, "C2")
+        out["blocking_polygonize_mpus_c3"] = blocking_contract(poly, "C3")
         bg = gpu.Group([device, device])
         try:
             bg.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
-            bg.set_option(gpu.GROUP_OPT_MIN_PART_MPUS, gpu.BLOCKING_MIN_PART_MPUS)  # as the drop-ins
+            bg.set_option(gpu.GROUP_OPT_MIN_PART_MPUS, gpu.BLOCKING_MIN_PART_MPUS)
             bg.set_option(gpu.OPT_JIT, args.jit)
-            out["blocking_polygonize_mpus"] = blocking_contract(bg, "C2")
-            out["blocking_polygonize_mpus_c3"] = blocking_contract(bg, "C3")
+            out["blocking_polygonize_mpus_c3_2parts"] = blocking_contract(bg, "C3")
         finally:
             bg.close()
-        out["blocking_polygonize_mpus_one_context"] = blocking_contract(poly, "C2")
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(model, cs, N ** 3, args.config)
     if grp.rank == 0:

@@ -69,14 +69,14 @@ private:
 };
 
 /* `parts` contexts on one device, each polygonizing a cost-balanced MPU range on a stream of
- * its own (psgpu_group over {device, ..., device}): a blocking caller's one polygonization
- * finishes sooner as 2 parts, whose kernel chains fill each other's tails (C3: 0.104 vs
- * 0.118 ms); the parts' meshes concatenate in range order to the one-context
- * mesh.  The split comes from a planning run of the lattice (PSGPU_GROUP_BALANCE_PLAN),
- * made once per cell size and scene box. */
-/* A part's smallest range for the blocking drop-ins: a lattice of fewer than 2 x this many
- * MPUs runs as one chain (C2, 6,859 MPUs: one context 0.049 ms vs 2 parts 0.058 for the
- * kernels; C3, 50,653: 0.114 vs 0.105 -- tools/blocking_breakdown.py). */
+ * its own (psgpu_group over {device, ..., device}): one polygonization's kernels finish
+ * sooner as 2 parts, whose kernel chains fill each other's tails (C3: 0.106 vs 0.114 ms,
+ * DESIGN.md §4) -- what SimdPolyT::run waits for; the parts' meshes concatenate in range
+ * order to the one-context mesh.  The split comes from a planning run of the lattice
+ * (PSGPU_GROUP_BALANCE_PLAN), made once per cell size and scene box. */
+/* A part's smallest range: a lattice of fewer than 2 x this many MPUs runs as one chain
+ * (C2, 6,859 MPUs: one context 0.048 ms vs 2 parts 0.058 for the kernels; C3, 50,653: 0.114
+ * vs 0.106 -- tools/blocking_breakdown.py). */
 constexpr uint32_t kBlockingMinPartMpus = 16384;
 
 class Group {
@@ -105,12 +105,6 @@ inline Context& default_context() {
     return ctx;
 }
 
-/* The calling thread's default blocking group: 2 parts on device 0. */
-inline Group& default_group() {
-    static thread_local Group g(0, 2);
-    return g;
-}
-
 /* CountMPUNeeded (PS_Polygonizer.h:384). */
 template <class Vec3>
 inline uint32_t CountMPUNeeded(float cellsize, const Vec3& lo, const Vec3& hi) {
@@ -128,9 +122,10 @@ inline int PrepareBBoxes(float cellsize, Prims& prims, BoxMats& boxMatrices, Ops
 
 /* Polygonize (PS_Polygonizer.h:386-391): fills polyMPUs.vMPUs[0..ctMPUs) and ctMPUs.
  * PolyMPUs is {MPU vMPUs[MAX_MPU_COUNT]; U32 ctMPUs;} (PS_Polygonizer.h:196-198);
- * MPUs that fail S1 get zero counts (the reference leaves them stale).  Without `ctx` it
- * runs on the calling thread's default 2-part group (default_group(): the shortest wait
- * for one polygonization); with `ctx`, on that one context. */
+ * MPUs that fail S1 get zero counts (the reference leaves them stale).  Runs on `ctx`, or
+ * on the calling thread's default context of device 0: one context is the faster whole
+ * call (C3 0.535 vs 0.612 ms on a 2-part group, whose shorter kernels do not make up for
+ * scattering two parts' downloads; DESIGN.md §4 "Blocking"). */
 template <class Prims, class Mats, class Ops, class PolyMPUsT>
 inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
                       void* lpProcessStats = nullptr, Context* ctx = nullptr) {
@@ -138,20 +133,12 @@ inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, cons
     (void)lpProcessStats;  // MPUSTATS is filled by the reference only under a compile flag
     const uint32_t capacity = (uint32_t)(sizeof(polyMPUs.vMPUs) / sizeof(polyMPUs.vMPUs[0]));
     uint32_t ct = 0;
-    int rc;
-    if (ctx) {
-        if (!ctx->ok()) return ctx->status();
-        rc = psgpu_polygonize_mpus(ctx->get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
-                                   detail::as_c<Mats, PsSoaPrimMatrices>(mats), detail::as_c<Ops, PsSoaBlobOps>(ops),
-                                   reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr);
-    } else {
-        Group& g = default_group();
-        if (!g.ok()) return g.status();
-        rc = psgpu_group_polygonize_mpus(g.get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
+    Context& c = ctx ? *ctx : default_context();
+    if (!c.ok()) return c.status();
+    const int rc = psgpu_polygonize_mpus(c.get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
                                          detail::as_c<Mats, PsSoaPrimMatrices>(mats),
                                          detail::as_c<Ops, PsSoaBlobOps>(ops),
-                                         reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct);
-    }
+                                         reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr);
     // on failure nothing was exported: report no MPUs (SimdPoly::draw walks ctMPUs,
     // PS_HighPerformanceRender.cpp:378-426, and must not draw stale ones)
     polyMPUs.ctMPUs = rc == PSGPU_RET_SUCCESS ? ct : 0u;

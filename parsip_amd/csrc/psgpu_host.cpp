@@ -561,19 +561,6 @@ int vertex_vpw(const psgpu_ctx* c) {
     return (uint64_t)c->lastV > 16u * waves && !c->alone ? 64 : 16;  // a lone run: the quad
 }
 
-// k_mpu's dynamic LDS: its per-MPU tables, or (PSGPU_MPU_BLOCKS_PER_CU=n, experiments) padded
-// to 1/n of the CU's 160 KB so at most n of its blocks are resident per CU
-size_t mpu_lds_launch(const psgpu_ctx* c) {
-    static const long perCu = [] {
-        const char* e = getenv("PSGPU_MPU_BLOCKS_PER_CU");
-        return e ? strtol(e, nullptr, 10) : 0L;
-    }();
-    (void)c;
-    const size_t base = mpu_lds_bytes(0);
-    if (perCu <= 0) return base;
-    return std::max(base, (size_t)(160 * 1024 / perCu) & ~(size_t)255);
-}
-
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
@@ -585,7 +572,7 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_launch(c), s, p));
+    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
@@ -1453,15 +1440,14 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
         PSGPU_CHECK(launch_export_meta(ms, hd, s));
     }
     PSGPU_CHECK(hipEventRecord(c->exportEv[0], s));
-    // the mesh packed piece by piece (MPU ranges of about 1 MB of mesh, at most 16) into one
-    // contiguous region by one kernel writing it over PCIe; the host scatter of one piece
-    // overlaps the transfer of the next
-    static const size_t pieceBytes = getenv("PSGPU_EXPORT_PIECE_KB") ? (size_t)atoi(getenv("PSGPU_EXPORT_PIECE_KB")) << 10 : kExportPieceBytes;  // A/B
+    // the mesh packed piece by piece (MPU ranges of about 1 MB of mesh, at most 16: C3 0.535 vs
+    // 0.570 ms with 2 MB) into one contiguous region by one kernel writing it over PCIe; the
+    // host scatter of one piece overlaps the transfer of the next
     // 256 blocks: one wave per SIMD keeps the link busy; 1,024 or 2,048 were 1.8-4.5x slower,
     // every block's per-piece release (an L2 write-back) adding up (r04)
     S.packBlocks = kExportPackBlocks;
     S.pieces = (int)std::min<size_t>({(size_t)kExportPieces, std::max<size_t>(N, 1),
-                                      1 + 4 * pack_words(V, T) / pieceBytes});
+                                      1 + 4 * pack_words(V, T) / kExportPieceBytes});
     if (S.meshBytes && N) {
         PackSrc src{c->offs, c->pos, c->nrm, c->col, c->tris, (uint32_t)N, (uint32_t)S.pieces,
                     reinterpret_cast<uint32_t*>(hd + S.oFlags), S.epoch, S.packBlocks};
@@ -1586,13 +1572,12 @@ int ScatterJob::finish(PsMpuStats* stats) {
 
 // The scatter is bound by the write-allocates of the sparse PolyMPUs layout (21.5 KB per MPU):
 // several host threads, as the reference's TBB bodies fill it -- about one per 256 KB of mesh,
-// at most 16, kept in c's pool.  Runs jobs[0..n) in one pass: every thread takes its chunks of
+// at most 16 (C3 0.535 vs 0.586 ms with 8), kept in c's pool.  Runs jobs[0..n) in one pass: every thread takes its chunks of
 // each job in turn.
 int scatter_jobs(psgpu_ctx* c, ScatterJob* jobs, size_t n) {
     size_t bytes = 0;
     for (size_t j = 0; j < n; ++j) bytes += jobs[j].active ? jobs[j].S->meshBytes : 0;
-    static const size_t maxTh = getenv("PSGPU_SCATTER_THREADS") ? (size_t)atoi(getenv("PSGPU_SCATTER_THREADS")) : 16;  // A/B
-    const unsigned nth = (unsigned)std::min<size_t>({maxTh, std::max(1u, std::thread::hardware_concurrency()),
+    const unsigned nth = (unsigned)std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()),
                                                     1 + bytes / (256 << 10)});
     std::function<void(unsigned)> task = [&](unsigned k) {
         for (size_t j = 0; j < n; ++j) jobs[j].task(k, nth);

@@ -439,23 +439,15 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
     """Blocking drop-in for PS::SIMDPOLY::Polygonize.
 
     Fills ``poly_mpus`` (a MPU_DTYPE array, default capacity MAX_MPU_COUNT as in PolyMPUs)
-    and returns ``(code, ctMPUs, poly_mpus)``.  Runs on this process's default 2-part group
-    of the device (the shortest wait for one polygonization, as parsip_gpu.hpp's
-    psgpu::Polygonize); with ``stats`` (per-MPU PsMpuStats) on one context.
+    and returns ``(code, ctMPUs, poly_mpus)``.  Runs on this process's default context of the
+    device, as parsip_gpu.hpp's psgpu::Polygonize (one context is the faster whole call;
+    DESIGN.md §4 "Blocking"); ``stats`` receives per-MPU PsMpuStats.
     """
     if model.ct_prims == 0:
         return soa.RET_PARAM_ERROR, 0, poly_mpus
-    if stats is not None:
-        if device not in _DEFAULT:
-            _DEFAULT[device] = Polygonizer(device)
-        return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats)
-    key = ("group", device)
-    if key not in _DEFAULT:
-        g = Group([device, device])
-        g.set_option(GROUP_OPT_BALANCE, BALANCE_PLAN)
-        g.set_option(GROUP_OPT_MIN_PART_MPUS, BLOCKING_MIN_PART_MPUS)
-        _DEFAULT[key] = g
-    return _DEFAULT[key].polygonize_mpus(cellsize, model, poly_mpus)
+    if device not in _DEFAULT:
+        _DEFAULT[device] = Polygonizer(device)
+    return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats)
 
 
 def _mesh_from_arrays(V, T, N, fill):
