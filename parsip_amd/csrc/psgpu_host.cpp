@@ -26,6 +26,7 @@
 #include "psgpu_internal.h"
 #include "psgpu_launch.h"
 
+
 using namespace psgpu;
 
 namespace {
@@ -1485,27 +1486,45 @@ int ScatterJob::prepare(psgpu_ctx* ctx, const ExportStage& st, PsMPU* out) {
 }
 
 // piece k is in when every block of k_export_pack has raised its flag for it; the kernel's
-// event ends the wait should it fail
-bool ScatterJob::wait_piece(int k) const {
-    const uint32_t* f = flags + (size_t)k * S->packBlocks;
-    uint32_t b = 0;
+// event ends the wait should it fail.  One thread at a time reads the flags (they sit in
+// memory the device writes over PCIe: sixteen threads polling them slowed the device's
+// writes in some calls) and publishes the count of pieces in; the others watch that count.
+bool ScatterJob::wait_piece(int k) {
     for (uint32_t spin = 1;; ++spin) {
-        while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
-        if (b == S->packBlocks) return true;
-        if ((spin & 255) == 0) {
-            const hipError_t e = hipEventQuery(c->exportEv[1]);
-            if (e == hipSuccess) {  // the kernel is done: every flag must be up now
+        const int r = ready.load(std::memory_order_acquire);
+        if (r > k) return true;
+        if (r < 0) return false;  // the kernel failed
+        bool idle = false;
+        if (polling.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
+            int n = ready.load(std::memory_order_acquire);
+            while (n >= 0 && n < S->pieces) {  // advance over every piece already in
+                const uint32_t* f = flags + (size_t)n * S->packBlocks;
+                uint32_t b = 0;
                 while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
-                return b == S->packBlocks;
+                if (b < S->packBlocks) {
+                    if ((spin & 63) == 0) {
+                        const hipError_t e = hipEventQuery(c->exportEv[1]);
+                        if (e != hipErrorNotReady) {  // done (every flag must be up) or failed
+                            while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
+                            if (e != hipSuccess || b < S->packBlocks) n = -1;
+                            else ++n;
+                            ready.store(n, std::memory_order_release);
+                            continue;
+                        }
+                    }
+                    break;
+                }
+                ready.store(++n, std::memory_order_release);
             }
-            if (e != hipErrorNotReady) return false;
+            polling.store(false, std::memory_order_release);
+            for (int i = 0; i < 256; ++i) __builtin_ia32_pause();  // ~1-2 us between reads of the flags
         }
         std::this_thread::yield();
     }
 }
 
 // MPUs [lb, le) into PolyMPUs (Polygonize :360-371); `have` = the pieces this thread has seen in
-bool ScatterJob::range(uint32_t lb, uint32_t le, int* have) const {
+bool ScatterJob::range(uint32_t lb, uint32_t le, int* have) {
     int k = 0;
     while (k + 1 < S->pieces && lb >= pm[k + 1]) ++k;
     for (uint32_t l = lb; l < le; ++l) {
@@ -1582,15 +1601,18 @@ int scatter_jobs(psgpu_ctx* c, ScatterJob* jobs, size_t n) {
     std::function<void(unsigned)> task = [&](unsigned k) {
         for (size_t j = 0; j < n; ++j) jobs[j].task(k, nth);
     };
-    if (nth > 1 && (!c->scatterPool || c->scatterPool->workers() + 1 < nth)) {
+    // nth workers on the caller's NUMA node; the caller only waits
+    if (nth > 1 && (!c->scatterPool || c->scatterPool->workers() < nth)) {
         c->scatterPool.reset();
         try {
-            c->scatterPool.reset(new ScatterPool(nth - 1));
+            cpu_set_t node;
+            const bool haveNode = ScatterPool::caller_node_cpus(&node);
+            c->scatterPool.reset(new ScatterPool(nth, haveNode ? &node : nullptr));
         } catch (...) {  // no threads to be had: this caller scatters alone
             c->scatterPool.reset();
         }
     }
-    if (nth > 1 && c->scatterPool) c->scatterPool->run(nth, task);
+    if (nth > 1 && c->scatterPool) c->scatterPool->run(nth, task, false);
     else
         for (unsigned k = 0; k < nth; ++k) task(k);
     return PSGPU_RET_SUCCESS;

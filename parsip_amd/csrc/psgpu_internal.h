@@ -178,8 +178,10 @@ struct ScatterJob {
     uint32_t pm[kExportPieces + 1] = {};
     size_t pbase[kExportPieces] = {}, pv0[kExportPieces] = {}, pt0[kExportPieces] = {}, pnv[kExportPieces] = {};
     int prepare(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus);
-    bool wait_piece(int k) const;
-    bool range(uint32_t lb, uint32_t le, int* have) const;
+    std::atomic<int> ready{0};        // pieces known to be in (-1: the packing kernel failed)
+    std::atomic<bool> polling{false};  // a thread is reading the flags
+    bool wait_piece(int k);
+    bool range(uint32_t lb, uint32_t le, int* have);
     void task(unsigned k, unsigned nth);
     int finish(PsMpuStats* stats);
 };

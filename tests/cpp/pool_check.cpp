@@ -7,8 +7,10 @@
 #include "psgpu_pool.h"
 
 int main() {
-    for (unsigned workers : {1u, 3u, 15u}) {
-        psgpu::ScatterPool pool(workers);
+    cpu_set_t node;
+    const bool haveNode = psgpu::ScatterPool::caller_node_cpus(&node);
+    for (unsigned workers : {1u, 3u, 16u}) {
+        psgpu::ScatterPool pool(workers, haveNode && workers == 16 ? &node : nullptr);
         std::vector<std::atomic<int>> hits(16);
         for (int run = 0; run < 20000; ++run) {
             const unsigned n = 1 + (unsigned)(run * 7) % 16;
@@ -20,7 +22,7 @@ int main() {
                 hits[k].fetch_add(1);
                 inside.fetch_sub(1);
             };
-            pool.run(n, f);
+            pool.run(n, f, run % 2 == 0);  // the caller draining or only waiting
             if (inside.load() != 0) {
                 std::printf("run %d returned with a task in flight\n", run);
                 return 1;
