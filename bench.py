@@ -889,7 +889,7 @@ def main():
         out["latency_ms_single_parts"] = latency_single_parts(device, model, cs, args.jit)
         # the drop-ins' blocking contract (psgpu::Polygonize / gpu.Polygonize: one context), C2
         # and the headline's C3; beside it C3 on a 2-part group of the device (shorter kernels,
-        # slower export: DESIGN.md §4 "Blocking")
+        # the same whole call: DESIGN.md §4 "Blocking")
         out["blocking_polygonize_mpus"] = blocking_contract(poly, "C2")
         out["blocking_polygonize_mpus_c3"] = blocking_contract(poly, "C3")
         bg = gpu.Group([device, device])

@@ -123,9 +123,8 @@ inline int PrepareBBoxes(float cellsize, Prims& prims, BoxMats& boxMatrices, Ops
 /* Polygonize (PS_Polygonizer.h:386-391): fills polyMPUs.vMPUs[0..ctMPUs) and ctMPUs.
  * PolyMPUs is {MPU vMPUs[MAX_MPU_COUNT]; U32 ctMPUs;} (PS_Polygonizer.h:196-198);
  * MPUs that fail S1 get zero counts (the reference leaves them stale).  Runs on `ctx`, or
- * on the calling thread's default context of device 0: one context is the faster whole
- * call (C3 0.535 vs 0.612 ms on a 2-part group, whose shorter kernels do not make up for
- * scattering two parts' downloads; DESIGN.md §4 "Blocking"). */
+ * on the calling thread's default context of device 0 (C3 0.53 ms end to end; a 2-part
+ * group's whole call measures the same, DESIGN.md §4 "Blocking"). */
 template <class Prims, class Mats, class Ops, class PolyMPUsT>
 inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
                       void* lpProcessStats = nullptr, Context* ctx = nullptr) {

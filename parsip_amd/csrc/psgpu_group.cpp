@@ -458,7 +458,11 @@ int psgpu_group_export_polympus(psgpu_group* g, PsMPU* mpus, uint32_t capacity, 
     std::vector<ExportStage> st(g->parts.size());
     for (size_t p = 0; p < g->parts.size(); ++p) {
         rc = set_device(g->parts[p]);
-        if (rc == PSGPU_RET_SUCCESS) rc = export_stage(g->parts[p], true, false, &st[p]);
+        // parts on one device share its link: each part's packing waits for the previous
+        // part's, so the pieces arrive in range order, as the scatter threads take them
+        hipEvent_t after =
+            p > 0 && g->parts[p - 1]->device == g->parts[p]->device ? g->parts[p - 1]->exportEv[1] : nullptr;
+        if (rc == PSGPU_RET_SUCCESS) rc = export_stage(g->parts[p], true, false, &st[p], after);
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
     // then one pass of the first part's scatter threads over every part, in range order per

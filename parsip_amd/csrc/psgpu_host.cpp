@@ -1395,7 +1395,7 @@ namespace psgpu {
 // (export_scatter).  Pageable destinations would cost a staged copy and a wait each (7 of
 // them for a mesh plus statistics).  A group stages every part before it scatters the first,
 // so the later parts' copies overlap the earlier parts' scatter.  Call after psgpu_finish.
-int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
+int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_t after) {
     const PsMeshInfo& I = c->info;
     ExportStage& S = *st;
     S.mesh = mesh;
@@ -1449,6 +1449,7 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st) {
     S.packBlocks = kExportPackBlocks;
     S.pieces = (int)std::min<size_t>({(size_t)kExportPieces, std::max<size_t>(N, 1),
                                       1 + 4 * pack_words(V, T) / kExportPieceBytes});
+    if (after) PSGPU_CHECK(hipStreamWaitEvent(s, after, 0));
     if (S.meshBytes && N) {
         PackSrc src{c->offs, c->pos, c->nrm, c->col, c->tris, (uint32_t)N, (uint32_t)S.pieces,
                     reinterpret_cast<uint32_t*>(hd + S.oFlags), S.epoch, S.packBlocks};

@@ -160,7 +160,9 @@ struct ExportStage {
     size_t oMesh = 0, meshBytes = 0, oFlags = 0;
     uint32_t epoch = 0, packBlocks = 0;
 };
-int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st);
+// `after`: an event the packing kernel waits for (the previous part's packing on the same
+// device, so the parts' pieces cross the link in range order)
+int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_t after = nullptr);
 int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats);
 // One staged export's scatter into PolyMPUs, split so that a group's parts go in one pass of
 // the thread pool (scatter_jobs): prepare (after the metadata), task per thread, finish.

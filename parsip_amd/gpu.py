@@ -440,8 +440,8 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
 
     Fills ``poly_mpus`` (a MPU_DTYPE array, default capacity MAX_MPU_COUNT as in PolyMPUs)
     and returns ``(code, ctMPUs, poly_mpus)``.  Runs on this process's default context of the
-    device, as parsip_gpu.hpp's psgpu::Polygonize (one context is the faster whole call;
-    DESIGN.md §4 "Blocking"); ``stats`` receives per-MPU PsMpuStats.
+    device, as parsip_gpu.hpp's psgpu::Polygonize (a 2-part group's whole call measures the
+    same; DESIGN.md §4 "Blocking"); ``stats`` receives per-MPU PsMpuStats.
     """
     if model.ct_prims == 0:
         return soa.RET_PARAM_ERROR, 0, poly_mpus
