@@ -178,6 +178,28 @@ def test_group_export_polympus_equals_single_context(group8, gpu_poly):
     assert e.value.code == -4
 
 
+def test_group_blocking_c3_two_parts_equals_single_context(gpu_poly):
+    """The blocking export at C3 (several ~1 MB pieces per part, the second part's packing
+    queued behind the first's, one pass of the scatter threads over both parts) fills PolyMPUs
+    byte for byte as one context does, call after call."""
+    model, cs, _ = synth.make_config("C3")
+    n = gpu.count_mpus(cs, *model.bbox)
+    g = gpu.Group([0, 0])
+    try:
+        g.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
+        a = np.zeros(n, soa.MPU_DTYPE)
+        b = np.zeros(n, soa.MPU_DTYPE)
+        for _ in range(2):
+            rc, ct, _ = g.polygonize_mpus(cs, model, a)
+            assert rc == soa.RET_SUCCESS and ct == n
+            rc, ct, _ = gpu_poly.polygonize_mpus(cs, model, b)
+            assert rc == soa.RET_SUCCESS and ct == n
+            assert a.tobytes() == b.tobytes()
+        assert int(b["ctTriangles"].sum()) == 520224
+    finally:
+        g.close()
+
+
 def test_rccl_exchange_single_rank(gpu_poly):
     """The RCCL path of the multi-process form at world size 1 (one GPU on this box)."""
     model, cs, _ = synth.make_config("C2")
