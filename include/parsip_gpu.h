@@ -142,6 +142,29 @@ typedef struct PsMpuStats {
     uint32_t ctTriangles;
 } PsMpuStats;
 
+/* MPUSTATS (PS_Polygonizer.h:201-207) in the reference's LP64 layout: int idxThread,
+ * int bIntersected, tbb_thread::id threadID (a pthread_t), tbb::tick_count tickStart,
+ * tickEnd (one long long each: legacy TBB's tick_count::now() on Linux is CLOCK_REALTIME in
+ * nanoseconds).  CMPUProcessor::operator() (.cpp:449-461) writes threadID, tickStart and
+ * tickEnd of every MPU and leaves idxThread / bIntersected alone; so does the library
+ * (psgpu_download_process_stats):
+ *   tickStart  the start of the wavefront that ran the MPU's S1 (k_precheck),
+ *   tickEnd    the end of the wavefront that ran its S2-S3 and made its vertex / triangle
+ *              records (k_mpu), or of its S1 wave when no S2 was needed (S1 failed, or field
+ *              bounds proved it surface-free); S4-S6 run batched over every MPU's records in
+ *              k_vertex / k_finish (psgpu_last_kernel_times gives their spans),
+ *   threadID   the hardware slot of that last wave: XCC_ID << 16 | HW_ID[15:0] (wave slot,
+ *              SIMD, CU, SH, SE), the device's "thread",
+ * both ticks in CLOCK_REALTIME nanoseconds, mapped from the device clock (s_memrealtime)
+ * by bracketing one device clock reading with the host clock (a few microseconds). */
+typedef struct PsMpuProcessStats {
+    int32_t  idxThread;
+    int32_t  bIntersected;
+    uint64_t threadID;
+    int64_t  tickStart;
+    int64_t  tickEnd;
+} PsMpuProcessStats;
+
 /* Result summary of one polygonization. */
 typedef struct PsMeshInfo {
     uint32_t ctMPUs;            /* MPUs in the processed range                     */
@@ -221,6 +244,17 @@ int  psgpu_polygonize_mpus(psgpu_ctx* ctx, float cellsize, const PsSoaBlobPrims*
                            const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops,
                            PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs,
                            PsMpuStats* statsOrNull);
+/* The same with the reference's MPUSTATS* lpProcessStats (Polygonize :386-391, :379): when
+ * processStats is not NULL the run records per-MPU ticks (PSGPU_OPT_MPU_TICKS for this call)
+ * and processStats[0..ctMPUs) receives them as psgpu_download_process_stats gives them. */
+int  psgpu_polygonize_mpus_ex(psgpu_ctx* ctx, float cellsize, const PsSoaBlobPrims* prims,
+                              const PsSoaPrimMatrices* matrices, const PsSoaBlobOps* ops,
+                              PsMPU* mpus, uint32_t capacity, uint32_t* outCtMPUs,
+                              PsMpuStats* statsOrNull, PsMpuProcessStats* processStatsOrNull);
+/* MPUSTATS of the last run (ctMPUs entries; threadID, tickStart, tickEnd written, the other
+ * fields untouched, as the reference).  PSGPU_RET_PARAM_ERROR if that run did not record
+ * ticks (PSGPU_OPT_MPU_TICKS was 0 when it was enqueued). */
+int  psgpu_download_process_stats(psgpu_ctx* ctx, PsMpuProcessStats* out);
 /* Per-wave timeline of the last polygonize (PSGPU_OPT_STAMPS > 0; the reference's
  * MPUSTATS / PrintThreadResults, PS_Polygonizer.h:201-207, .cpp:414-461, with waves for
  * threads): 4 kernels (precheck, mpu, vertex, finish) x cap records of 3 uint64:
@@ -245,7 +279,11 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_CULLING       2   /* 1: exact per-wave primitive culling (default) */
 #define PSGPU_OPT_DEBUG         9   /* profiling ablations (bit 0: stop after S2); 0 in use;
                                        bit 20 (test hook): the next run's k_mpu grid is one
-                                       block, so finish must re-run it with the full grid */
+                                       block, so finish must re-run it with the full grid;
+                                       bits 23 / 24 (test hooks of the blocking export): the
+                                       staging past the piece flags is filled with the call's
+                                       epoch before the export / the packing kernel's last
+                                       block waits ~40 us before each piece */
 #define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU */
 #define PSGPU_OPT_FINISH_BLOCKS_PER_CU 5  /* persistent k_finish grid */
 #define PSGPU_OPT_GRAPH         7   /* 1: replay repeated launch sequences from a hipGraph (off by
@@ -292,6 +330,8 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        whole tree.  Non-zero compiles the split kernels too (+30-45 %
                                        hiprtc time).  Identical output */
 #define PSGPU_OPT_SPLIT_MAX_QUEUED 17  /* threshold of PSGPU_OPT_TREE_SPLIT 2 (default 4 per CU) */
+#define PSGPU_OPT_MPU_TICKS    19   /* 1: runs record per-MPU ticks for MPUSTATS
+                                       (psgpu_download_process_stats); 0 (default) off */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the
                                        specialised kernels on a host thread while the interpreter
                                        serves polygonizations (bit-identical output); 0: block */
@@ -426,6 +466,10 @@ static_assert(offsetof(PsMPU, triangles) == 18432, "triangles offset");
 static_assert(offsetof(PsMPU, ctVertices) == 21504, "ctVertices offset");
 static_assert(offsetof(PsMPU, bboxLo) == 21508, "MPU bboxLo offset");
 static_assert(offsetof(PsMPU, ctFieldEvals) == 21520, "ctFieldEvals offset");
+static_assert(sizeof(PsMpuProcessStats) == 32, "MPUSTATS size (LP64)");
+static_assert(offsetof(PsMpuProcessStats, threadID) == 8, "MPUSTATS threadID offset");
+static_assert(offsetof(PsMpuProcessStats, tickStart) == 16, "MPUSTATS tickStart offset");
+static_assert(offsetof(PsMpuProcessStats, tickEnd) == 24, "MPUSTATS tickEnd offset");
 #else
 _Static_assert(sizeof(PsSoaBlobPrims) == 9500, "SOABlobPrims size");
 _Static_assert(sizeof(PsSoaBlobOps) == 5636, "SOABlobOps size");

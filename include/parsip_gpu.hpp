@@ -120,28 +120,57 @@ inline int PrepareBBoxes(float cellsize, Prims& prims, BoxMats& boxMatrices, Ops
                                 detail::as_c_mut<Ops, PsSoaBlobOps>(ops));
 }
 
-/* Polygonize (PS_Polygonizer.h:386-391): fills polyMPUs.vMPUs[0..ctMPUs) and ctMPUs.
- * PolyMPUs is {MPU vMPUs[MAX_MPU_COUNT]; U32 ctMPUs;} (PS_Polygonizer.h:196-198);
- * MPUs that fail S1 get zero counts (the reference leaves them stale).  Runs on `ctx`, or
- * on the calling thread's default context of device 0 (C3 0.53 ms end to end; a 2-part
- * group's whole call measures the same, DESIGN.md §4 "Blocking"). */
+namespace detail {
 template <class Prims, class Mats, class Ops, class PolyMPUsT>
-inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
-                      void* lpProcessStats = nullptr, Context* ctx = nullptr) {
+inline int polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
+                      PsMpuProcessStats* processStats, Context* ctx) {
     static_assert(sizeof(polyMPUs.vMPUs[0]) == sizeof(PsMPU), "MPU layout");
-    (void)lpProcessStats;  // MPUSTATS is filled by the reference only under a compile flag
     const uint32_t capacity = (uint32_t)(sizeof(polyMPUs.vMPUs) / sizeof(polyMPUs.vMPUs[0]));
     uint32_t ct = 0;
     Context& c = ctx ? *ctx : default_context();
     if (!c.ok()) return c.status();
-    const int rc = psgpu_polygonize_mpus(c.get(), cellsize, detail::as_c<Prims, PsSoaBlobPrims>(prims),
-                                         detail::as_c<Mats, PsSoaPrimMatrices>(mats),
-                                         detail::as_c<Ops, PsSoaBlobOps>(ops),
-                                         reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr);
+    const int rc = psgpu_polygonize_mpus_ex(c.get(), cellsize, as_c<Prims, PsSoaBlobPrims>(prims),
+                                            as_c<Mats, PsSoaPrimMatrices>(mats), as_c<Ops, PsSoaBlobOps>(ops),
+                                            reinterpret_cast<PsMPU*>(&polyMPUs.vMPUs[0]), capacity, &ct, nullptr,
+                                            processStats);
     // on failure nothing was exported: report no MPUs (SimdPoly::draw walks ctMPUs,
     // PS_HighPerformanceRender.cpp:378-426, and must not draw stale ones)
     polyMPUs.ctMPUs = rc == PSGPU_RET_SUCCESS ? ct : 0u;
     return rc;
+}
+}  // namespace detail
+
+/* Polygonize (PS_Polygonizer.h:386-391): fills polyMPUs.vMPUs[0..ctMPUs) and ctMPUs.
+ * PolyMPUs is {MPU vMPUs[MAX_MPU_COUNT]; U32 ctMPUs;} (PS_Polygonizer.h:196-198);
+ * MPUs that fail S1 get zero counts (the reference leaves them stale).  Runs on `ctx`, or
+ * on the calling thread's default context of device 0 (DESIGN.md §4 "Blocking").
+ * Without lpProcessStats (omitted, NULL or nullptr) no ticks are recorded. */
+template <class Prims, class Mats, class Ops, class PolyMPUsT>
+inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
+                      std::nullptr_t lpProcessStats = nullptr, Context* ctx = nullptr) {
+    (void)lpProcessStats;
+    return detail::polygonize(cellsize, prims, mats, ops, polyMPUs, nullptr, ctx);
+}
+/* With the reference's MPUSTATS* lpProcessStats (PS_Polygonizer.h:201-207; handed to
+ * CMPUProcessor, .cpp:379, which writes threadID / tickStart / tickEnd of every MPU,
+ * .cpp:449-461): lpProcessStats[0..ctMPUs) receives them as parsip_gpu.h's
+ * PsMpuProcessStats describes (ticks in tbb::tick_count's CLOCK_REALTIME nanoseconds, the
+ * device wave's hardware slot as the thread id; idxThread / bIntersected untouched).  The
+ * caller's struct is checked against that layout member by member at compile time. */
+template <class Prims, class Mats, class Ops, class PolyMPUsT, class MpuStatsT>
+inline int Polygonize(float cellsize, const Prims& prims, const Mats& mats, const Ops& ops, PolyMPUsT& polyMPUs,
+                      MpuStatsT* lpProcessStats, Context* ctx = nullptr) {
+    static_assert(!std::is_void<MpuStatsT>::value, "pass an MPUSTATS* (PS_Polygonizer.h:201-207), not a void*");
+    static_assert(sizeof(MpuStatsT) == sizeof(PsMpuProcessStats), "MPUSTATS size differs from the LP64 layout");
+    static_assert(offsetof(MpuStatsT, idxThread) == 0 && offsetof(MpuStatsT, bIntersected) == 4 &&
+                      offsetof(MpuStatsT, threadID) == 8 && offsetof(MpuStatsT, tickStart) == 16 &&
+                      offsetof(MpuStatsT, tickEnd) == 24,
+                  "MPUSTATS member offsets");
+    static_assert(sizeof(lpProcessStats->threadID) == 8 && sizeof(lpProcessStats->tickStart) == 8 &&
+                      sizeof(lpProcessStats->tickEnd) == 8,
+                  "MPUSTATS: 8-byte thread id and ticks (pthread_t, tick_count)");
+    return detail::polygonize(cellsize, prims, mats, ops, polyMPUs,
+                              reinterpret_cast<PsMpuProcessStats*>(lpProcessStats), ctx);
 }
 
 /* SimdPoly-shaped adapter (PS_HighPerformanceRender.h:15-33) over a device-resident
@@ -491,6 +520,7 @@ typedef PsSoaBlobOps SOABlobOps;
 typedef PsSoaPrimMatrices SOABlobPrimMatrices;
 typedef PsSoaBoxMatrices SOABlobBoxMatrices;
 typedef PsMPU MPU;
+typedef PsMpuProcessStats MPUSTATS;  /* PS_Polygonizer.h:201-207, LP64 layout (parsip_gpu.h) */
 struct PolyMPUs {  /* PS_Polygonizer.h:196-198 */
     MPU vMPUs[PSGPU_MAX_MPU_COUNT];
     uint32_t ctMPUs;

@@ -738,11 +738,37 @@ __device__ __forceinline__ void span_end(const Params& p, int K, uint64_t t0) {
         atomicMax(reinterpret_cast<unsigned long long*>(s + 1), (unsigned long long)t1);
     }
 }
+// The reference's per-MPU MPUSTATS ticks (PS_Polygonizer.cpp:449-461: tickStart / tickEnd
+// around process_cells_simd, the thread id), PSGPU_OPT_MPU_TICKS: the wave that ran S1 for
+// the MPU records its start and end (k_precheck, lane g < 8 of the brick's MPU g), the wave
+// that ran S2-S3 and made its vertex / triangle records raises the end (k_mpu).
+__device__ __forceinline__ uint32_t wave_hw_id() {
+    const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 15u;
+    return (hw & 0xffffu) | (xcc << 16);
+}
+__device__ __forceinline__ void mpu_ticks_s1(const Params& p, uint32_t w, uint64_t t0) {
+    uint64_t* r = p.mpuTicks + 4 * (size_t)w;
+    r[0] = t0;
+    r[1] = stamp_now();
+    r[2] = 0ull;
+    r[3] = (uint64_t)wave_hw_id();
+}
+__device__ __forceinline__ void mpu_ticks_s2(const Params& p, uint32_t m) {
+    const uint64_t t = stamp_now();
+    const uint32_t hw = wave_hw_id();
+    if (lane_id() == 0) {
+        uint64_t* r = p.mpuTicks + 4 * (size_t)(m - p.mpuBegin);
+        atomicMax(reinterpret_cast<unsigned long long*>(r + 2), (unsigned long long)t);
+        reinterpret_cast<uint32_t*>(r + 3)[1] = hw;
+    }
+}
 #define PSGPU_STAMPED(K, ITEM, CALL)                                             \
     {                                                                             \
         const uint64_t t0_ = (p.stamps || p.spans) ? psgpu::stamp_now() : 0ull;  \
         uint32_t item_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);     \
         CALL;                                                                     \
+        if (K == 1 && p.mpuTicks && ITEM != 0xffffffffu) psgpu::mpu_ticks_s2(p, ITEM); \
         if (p.stamps) psgpu::stamp_end(p, K, t0_, ITEM);                          \
         if (p.spans) psgpu::span_end(p, K, t0_);                                  \
     }
@@ -789,6 +815,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int part = wave % SPLIT;  // subtree of the root this wave walks (SPLIT 2)
     const int slot = wave / SPLIT;  // the block's brick
     phase_stamp(p, 0, 8192u);
+    const uint64_t tick0 = p.mpuTicks ? stamp_now() : 0ull;  // MPUSTATS tickStart
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
     CullLanes cl;  // loaded first: independent of everything below
     if (p.cull) cl = load_cull_lanes(as_const(p.model));
@@ -926,6 +953,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
         // 0: failed S1; 1: passed, proven empty by field bounds; 2: passed, queued for S2
         p.passed[mOf - p.mpuBegin] = (uint8_t)(((flags8 >> lane) & 1u) + ((queue8 >> lane) & 1u));
         if (!pass) p.counts[mOf - p.mpuBegin] = 0ull;
+        if (p.mpuTicks) mpu_ticks_s1(p, mOf - p.mpuBegin, tick0);
     }
     if (flags8 == 0u) return;
     const uint32_t shard = W / (p.pShardCap / 8u);

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <functional>
 #include <limits>
 #include <memory>
@@ -450,6 +451,7 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     PSGPU_CHECK(grow(c->nrm, capV2, (size_t)c->vcap * 3));
     PSGPU_CHECK(grow(c->col, capV3, (size_t)c->vcap * 3));
     PSGPU_CHECK(grow(c->tris, c->capT, (size_t)c->tcap * 3));
+    if (c->mpuTicksOpt) PSGPU_CHECK(grow(c->mpuTicks, c->capTicks, 4 * n));
     return PSGPU_RET_SUCCESS;
 }
 
@@ -520,6 +522,7 @@ Params make_params(psgpu_ctx* c) {
     p.stampCap = c->stamps ? c->stampCap : 0u;
     p.spans = (c->spans && c->spanNext < c->spanCap)
                   ? c->spans + (size_t)c->spanNext * 2 * kNumStampKernels * kSpanLanes : nullptr;
+    p.mpuTicks = c->mpuTicksOpt ? c->mpuTicks : nullptr;
     p.slotsPerLane = c->jit ? 0u : c->model.nSlots;
     p.debug = (uint32_t)c->debug;
     return p;
@@ -601,6 +604,7 @@ void drop_graphs(psgpu_ctx* c) {
 void reset_run_state(psgpu_ctx* c);
 int enqueue(psgpu_ctx* c, hipStream_t s) {
     if (c->mpuCount == 0) {  // nothing to launch: an empty result
+        c->runTicks = c->mpuTicksOpt != 0;
         memset(c->hostCtr, 0, sizeof(DevCounters));
         c->hostCtr->firstOverflow = 0x7fffffff;
         // the totals the count exchange reads (k_finish writes them on a real run): zero
@@ -609,6 +613,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         return PSGPU_RET_SUCCESS;
     }
     const Params p = make_params(c);
+    c->runTicks = p.mpuTicks != nullptr;
     c->debug &= ~(1 << 20);  // the short-grid test hook applies to one run
     if (p.spans) c->spanNext++;
     c->runMpuBlocks = p.mpuBlocks;
@@ -991,10 +996,11 @@ void psgpu_destroy(psgpu_ctx* c) {
     c->jit.reset();
     c->jit1.reset();
     void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
-                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans};
+                    c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans, c->mpuTicks};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hostCtr) (void)hipHostFree(c->hostCtr);
+    if (c->clockProbe) (void)hipHostFree(c->clockProbe);
     if (c->hostStage) (void)hipHostFree(c->hostStage);
     for (int i = 0; i <= kNumKernels; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -1054,6 +1060,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         jit_start(c);
     }
     else if (option == PSGPU_OPT_JIT_ASYNC) c->jitAsync = value != 0;
+    else if (option == PSGPU_OPT_MPU_TICKS) c->mpuTicksOpt = value != 0;  // buffers: next polygonize
     else if (option == PSGPU_OPT_SPANS && value >= 0 && value <= (1 << 20)) {
         // the next `value` runs record their kernel spans, one slot each (then none)
         if (c->pending) (void)hipStreamSynchronize(c->runStream);
@@ -1349,6 +1356,66 @@ int psgpu_download_stats(psgpu_ctx* c, PsMpuStats* stats) {
     }
     return PSGPU_RET_SUCCESS;
 }
+// MPUSTATS (PS_Polygonizer.h:201-207, written at .cpp:449-461): the per-MPU device ticks of
+// the last run on the host's CLOCK_REALTIME nanosecond scale (legacy TBB's tick_count on
+// Linux).  The device clock (s_memrealtime, wall-clock rate from the runtime) is mapped by
+// bracketing one reading of it (k_clock_probe, stored straight into mapped host memory)
+// between two host readings; of 8 tries the tightest bracket gives the offset, which is then
+// good to half its width (a few microseconds; MPU ticks are tens of microseconds apart).
+int psgpu_download_process_stats(psgpu_ctx* c, PsMpuProcessStats* out) {
+    int rc = psgpu_finish(c, nullptr);
+    if (rc != PSGPU_RET_SUCCESS) return rc;
+    if (!out || !c->runTicks) return PSGPU_RET_PARAM_ERROR;
+    const uint32_t n = c->mpuCount;
+    if (!n) return PSGPU_RET_SUCCESS;
+    std::vector<uint64_t> t((size_t)n * 4);
+    PSGPU_CHECK(hipMemcpy(t.data(), c->mpuTicks, t.size() * 8, hipMemcpyDeviceToHost));
+    int khz = 0;
+    PSGPU_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    if (khz <= 0) return PSGPU_RET_DEVICE_ERROR;
+    if (!c->clockProbe)
+        PSGPU_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c->clockProbe), 64,
+                                  hipHostMallocMapped | hipHostMallocCoherent));
+    uint64_t* dProbe = nullptr;
+    PSGPU_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dProbe), c->clockProbe, 0));
+    auto host_ns = [] {
+        timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        return (int64_t)ts.tv_sec * 1000000000ll + (int64_t)ts.tv_nsec;
+    };
+    int64_t bestWidth = INT64_MAX, hostMid = 0;
+    uint64_t devAt = 0;
+    for (int k = 0; k < 8; ++k) {
+        __atomic_store_n(c->clockProbe, 0ull, __ATOMIC_RELEASE);
+        const int64_t h0 = host_ns();
+        PSGPU_CHECK(launch_clock_probe(dProbe, c->stream));
+        uint64_t d = 0;
+        for (uint64_t spin = 0; (d = __atomic_load_n(c->clockProbe, __ATOMIC_ACQUIRE)) == 0ull; ++spin)
+            if ((spin & 1023) == 1023 && hipStreamQuery(c->stream) != hipErrorNotReady) {
+                d = __atomic_load_n(c->clockProbe, __ATOMIC_ACQUIRE);
+                if (d == 0ull) return PSGPU_RET_DEVICE_ERROR;  // finished (or failed) without a reading
+                break;
+            }
+        const int64_t h1 = host_ns();
+        if (h1 - h0 < bestWidth) {
+            bestWidth = h1 - h0;
+            hostMid = h0 + (h1 - h0) / 2;
+            devAt = d;
+        }
+    }
+    PSGPU_CHECK(hipStreamSynchronize(c->stream));
+    const double nsPerTick = 1.0e6 / (double)khz;
+    auto to_ns = [&](uint64_t tick) { return hostMid + (int64_t)llround((double)((int64_t)(tick - devAt)) * nsPerTick); };
+    for (uint32_t l = 0; l < n; ++l) {
+        const uint64_t* r = &t[(size_t)4 * l];
+        const bool s2 = r[2] != 0ull;
+        out[l].threadID = s2 ? (r[3] >> 32) : (r[3] & 0xffffffffull);
+        out[l].tickStart = to_ns(r[0]);
+        out[l].tickEnd = to_ns(s2 ? r[2] : r[1]);
+    }
+    return PSGPU_RET_SUCCESS;
+}
+
 // Per-MPU work of the last run in lane-evaluations: 8 (S1) + 64 (field
 // bounds of a survivor) or 512 (S2 cache of a queued survivor) + 8 per vertex (4 root
 // samples, value and 3 normal samples).  Balances MPU ranges across devices.
@@ -1405,14 +1472,19 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_
     S.N = c->mpuCount;
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t N = S.N, V = S.V, T = S.T;
-    S.oOffs = 0;
-    S.oPass = up((N + 1) * 8);
+    // The per-piece flags sit at the front of the staging, at an offset no call moves: those
+    // words only ever hold flags (an older call's epoch, or 0), never mesh or offset words, so
+    // no stale word can equal this call's epoch (r04 kept them behind the mesh, where a call
+    // with a smaller mesh found the previous call's packed triangles and offsets -- ADVICE r04)
+    const size_t flagBytes = 4 * (size_t)kExportPieces * kExportPackBlocks;
+    S.oFlags = 0;
+    S.oOffs = up(flagBytes);
+    S.oPass = up(S.oOffs + (N + 1) * 8);
     S.oCnt = up(S.oPass + N);
     S.oMesh = up(S.oCnt + (stats ? N * 8 : 0));
     // the packed mesh: pack_words per piece; bounded by 4 extra words per piece
     S.meshBytes = mesh ? 4 * (pack_words(V, T) + 4 * kExportPieces) : 0;
-    S.oFlags = up(S.oMesh + S.meshBytes);
-    const size_t total = up(S.oFlags + 4 * (size_t)kExportPieces * kExportPackBlocks);
+    const size_t total = up(S.oMesh + S.meshBytes);
     if (total > c->hostStageCap) {
         if (c->hostStage) (void)hipHostFree(c->hostStage);
         c->hostStage = nullptr;
@@ -1430,6 +1502,11 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_
     }
     S.epoch = c->exportEpoch;
     unsigned char* h = c->hostStage;
+    if (c->debug & (1 << 23)) {  // test hook: every word past the flags reads as this call's epoch
+        // (the stream is idle: the previous export's scatter synchronised with it)
+        uint32_t* w = reinterpret_cast<uint32_t*>(h + flagBytes);
+        for (size_t i = 0, n = (c->hostStageCap - flagBytes) / 4; i < n; ++i) w[i] = S.epoch;
+    }
     hipStream_t s = c->stream;
     for (hipEvent_t& e : c->exportEv)
         if (!e) PSGPU_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1452,7 +1529,9 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_
     if (after) PSGPU_CHECK(hipStreamWaitEvent(s, after, 0));
     if (S.meshBytes && N) {
         PackSrc src{c->offs, c->pos, c->nrm, c->col, c->tris, (uint32_t)N, (uint32_t)S.pieces,
-                    reinterpret_cast<uint32_t*>(hd + S.oFlags), S.epoch, S.packBlocks};
+                    reinterpret_cast<uint32_t*>(hd + S.oFlags), S.epoch, S.packBlocks,
+                    // test hook: the last block waits ~40 us before each piece's share
+                    (c->debug & (1 << 24)) ? S.packBlocks - 1u : 0xffffffffu, 4000u};
         PSGPU_CHECK(launch_export_pack(src, reinterpret_cast<uint32_t*>(hd + S.oMesh), s));
     }
     PSGPU_CHECK(hipEventRecord(c->exportEv[1], s));
@@ -1675,6 +1754,20 @@ int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* pr
         return rc;
     }
     return export_blocking(c, mpus, capacity, outCt, stats);
+}
+
+int psgpu_polygonize_mpus_ex(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats,
+                             const PsSoaBlobOps* ops, PsMPU* mpus, uint32_t capacity, uint32_t* outCt,
+                             PsMpuStats* stats, PsMpuProcessStats* processStats) {
+    if (!c) return PSGPU_RET_PARAM_ERROR;
+    if (!processStats) return psgpu_polygonize_mpus(c, cellsize, prims, mats, ops, mpus, capacity, outCt, stats);
+    const int was = c->mpuTicksOpt;
+    c->mpuTicksOpt = 1;  // this call's run records the ticks (Polygonize :379 hands lpProcessStats on)
+    int rc = psgpu_polygonize_mpus(c, cellsize, prims, mats, ops, mpus, capacity, outCt, stats);
+    c->mpuTicksOpt = was;
+    // ctMPUs entries, as PolyMPUs: only on success (on -4 the caller's array may be shorter)
+    if (rc == PSGPU_RET_SUCCESS) rc = psgpu_download_process_stats(c, processStats);
+    return rc;
 }
 
 // Field probe (FieldComputer::fieldValue / fieldValueAndColor on arbitrary points).

@@ -115,6 +115,11 @@ struct psgpu_ctx {
     uint32_t stampCap = 0;
     uint64_t* spans = nullptr;          // per-run kernel spans (PSGPU_OPT_SPANS): spanCap x 4 x 2 words
     uint32_t spanCap = 0, spanNext = 0;
+    int mpuTicksOpt = 0;                // PSGPU_OPT_MPU_TICKS: runs record per-MPU ticks (MPUSTATS)
+    uint64_t* mpuTicks = nullptr;       // 4 words per MPU of the range (Params::mpuTicks)
+    size_t capTicks = 0;
+    bool runTicks = false;              // the last enqueued run recorded them
+    uint64_t* clockProbe = nullptr;     // pinned, mapped: one device clock reading (k_clock_probe)
     DevCounters* hostCtr = nullptr;     // pinned, mapped: written by k_finish
     DevCounters* hostCtrDev = nullptr;  // its device address
     unsigned char* hostStage = nullptr;  // pinned staging for the blocking PolyMPUs export
@@ -155,7 +160,7 @@ struct ExportStage {
     // the mesh, packed as `pieces` MPU ranges (pos | nrm | col | 16-bit triangle corners of
     // each, psgpu_launch.h PackSrc) at oMesh, piece k complete when its packBlocks flags at
     // oFlags + 4 k packBlocks equal epoch: the scatter of one piece overlaps the
-    // transfer of the next
+    // transfer of the next.  oFlags = 0 in every call: the flag words hold nothing else
     int pieces = 0;
     size_t oMesh = 0, meshBytes = 0, oFlags = 0;
     uint32_t epoch = 0, packBlocks = 0;

@@ -117,6 +117,10 @@ __global__ void __launch_bounds__(256) k_export_pack(PackSrc src, uint32_t* __re
             return (tri[e] - (uint32_t)src.offs[lo]) & 0xffffu;
         };
         uint32_t* out = dst + base;
+        if (blockIdx.x == src.delayBlock) {  // test hook: a straggling block (its share lands last)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < src.delayTicks) __builtin_amdgcn_s_sleep(32);
+        }
         for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
             uint32_t w;
             if (i < nv) w = pos[i];
@@ -201,6 +205,18 @@ __global__ void __launch_bounds__(256) k_export_meta(MetaSrc src, unsigned char*
 }
 hipError_t launch_export_meta(const MetaSrc& src, unsigned char* dst, hipStream_t s) {
     hipLaunchKernelGGL(k_export_meta, dim3(128), dim3(256), 0, s, src, dst);
+    return hipGetLastError();
+}
+
+// One reading of the device clock the kernels stamp with (s_memrealtime), stored into mapped
+// host memory: the host brackets it with its own clock to map device ticks to host time
+// (MPUSTATS, psgpu_download_process_stats).
+__global__ void __launch_bounds__(64) k_clock_probe(uint64_t* out) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) __hip_atomic_store(out, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t launch_clock_probe(uint64_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, s, out);
     return hipGetLastError();
 }
 

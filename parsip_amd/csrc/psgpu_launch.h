@@ -40,6 +40,8 @@ struct PackSrc {
     uint32_t n, pieces;
     uint32_t* flags;  // [pieces][blocks], set to epoch as each block finishes a piece
     uint32_t epoch, blocks;
+    uint32_t delayBlock;  // test hook (PSGPU_OPT_DEBUG bit 24): this block waits delayTicks of the
+    uint32_t delayTicks;  // 100 MHz device clock before each piece's share (0xffffffff: none)
 };
 constexpr uint32_t kExportPackBlocks = 256;
 hipError_t launch_export_pack(const PackSrc& src, uint32_t* dst, hipStream_t s);
@@ -51,5 +53,7 @@ struct MetaSrc {  // offs / counts null when not exported
     size_t oOffs, oPass, oCnt;  // byte offsets in dst
 };
 hipError_t launch_export_meta(const MetaSrc& src, unsigned char* dst, hipStream_t s);
+// *out (mapped host memory, device address) = the device clock (s_memrealtime) at one instant
+hipError_t launch_clock_probe(uint64_t* out, hipStream_t s);
 
 }  // namespace psgpu

@@ -244,6 +244,9 @@ struct Params {
     uint32_t stampCap;      // stampCap records {start, end, item | hw id << 32} (s_memrealtime)
     uint64_t* spans;        // PSGPU_OPT_SPANS: this run's slot, per kernel {first wave start, last
                             // wave end} (atomic min / max of s_memrealtime), or null
+    uint64_t* mpuTicks;     // PSGPU_OPT_MPU_TICKS (MPUSTATS): 4 words per MPU of the range -- its S1
+                            // wave's start and end, its S2 wave's end (0: not queued), hw ids of the
+                            // S1 | S2 waves << 32 (s_memrealtime) -- or null
     uint32_t slotsPerLane;  // value slots (x4 floats in colour mode)
     uint32_t debug;         // ablation switches for profiling (0 in production)
 };

@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_group_gather", "psgpu_group_export_polympus", "psgpu_group_polygonize_mpus",
     "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
     "psgpu_comm_result", "psgpu_download_stamps", "psgpu_comm_exchange_group", "psgpu_download_spans",
-    "psgpu_comm_reexchanged",
+    "psgpu_comm_reexchanged", "psgpu_polygonize_mpus_ex", "psgpu_download_process_stats",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -83,6 +83,9 @@ OPT_VERTEX_WIDE = 15
 OPT_TREE_SPLIT = 16
 OPT_SPLIT_MAX_QUEUED = 17
 OPT_TIER_RUNS = 18
+OPT_MPU_TICKS = 19
+DEBUG_EXPORT_POISON = 1 << 23  # test hooks of the blocking export (OPT_DEBUG bits)
+DEBUG_EXPORT_STRAGGLER = 1 << 24
 JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values
 STAMP_KERNELS = ("k_precheck", "k_mpu", "k_vertex", "k_finish")
 GROUP_OPT_BALANCE = 100
@@ -120,6 +123,8 @@ def load(build_if_missing: bool = True):
         "psgpu_download_stats": ([vp, vp], i32),
         "psgpu_export_polympus": ([vp, vp, u32, ctypes.POINTER(u32)], i32),
         "psgpu_polygonize_mpus": ([vp, f32, vp, vp, vp, vp, u32, ctypes.POINTER(u32), vp], i32),
+        "psgpu_polygonize_mpus_ex": ([vp, f32, vp, vp, vp, vp, u32, ctypes.POINTER(u32), vp, vp], i32),
+        "psgpu_download_process_stats": ([vp, vp], i32),
         "psgpu_last_kernel_times": ([vp, vp, i32, vp], i32),
         "psgpu_field_values": ([vp, vp, u32, i32, vp, vp], i32),
         "psgpu_set_option": ([vp, i32, ctypes.c_int64], i32),
@@ -374,18 +379,29 @@ class Polygonizer:
         return out[:ct.value]
 
     def polygonize_mpus(self, cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None = None,
-                        stats: np.ndarray | None = None):
-        """psgpu_polygonize_mpus on this context: the reference's blocking Polygonize (model
-        upload, run, download and scatter into the caller's PolyMPUs).  Returns
-        ``(code, ctMPUs, poly_mpus)``."""
+                        stats: np.ndarray | None = None, process_stats: np.ndarray | None = None):
+        """psgpu_polygonize_mpus(_ex) on this context: the reference's blocking Polygonize (model
+        upload, run, download and scatter into the caller's PolyMPUs).  ``process_stats``: the
+        reference's MPUSTATS* (a MPUSTATS_DTYPE array of at least ctMPUs records; threadID,
+        tickStart, tickEnd written).  Returns ``(code, ctMPUs, poly_mpus)``."""
         if poly_mpus is None:
             poly_mpus = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
         ct = ctypes.c_uint32()
         p, m, o = model.ptrs()
-        rc = self._L.psgpu_polygonize_mpus(self._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
-                                           ctypes.byref(ct), None if stats is None else stats.ctypes.data)
+        if process_stats is not None:
+            assert process_stats.dtype == soa.MPUSTATS_DTYPE and len(process_stats) >= len(poly_mpus)
+        rc = self._L.psgpu_polygonize_mpus_ex(self._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
+                                              ctypes.byref(ct), None if stats is None else stats.ctypes.data,
+                                              None if process_stats is None else process_stats.ctypes.data)
         self.model = model
         return rc, ct.value, poly_mpus
+
+    def process_stats(self) -> np.ndarray:
+        """MPUSTATS of the last run (it must have run with OPT_MPU_TICKS set)."""
+        info = self.finish()
+        st = np.zeros(max(info.ctMPUs, 1), soa.MPUSTATS_DTYPE)
+        _check(self._L.psgpu_download_process_stats(self._ctx, st.ctypes.data), "psgpu_download_process_stats")
+        return st[:info.ctMPUs]
 
     def device_mesh(self) -> PsMeshDevice:
         d = PsMeshDevice()
@@ -435,19 +451,20 @@ _DEFAULT = {}
 
 
 def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None = None, device: int = 0,
-               stats: np.ndarray | None = None):
+               stats: np.ndarray | None = None, process_stats: np.ndarray | None = None):
     """Blocking drop-in for PS::SIMDPOLY::Polygonize.
 
     Fills ``poly_mpus`` (a MPU_DTYPE array, default capacity MAX_MPU_COUNT as in PolyMPUs)
     and returns ``(code, ctMPUs, poly_mpus)``.  Runs on this process's default context of the
     device, as parsip_gpu.hpp's psgpu::Polygonize (a 2-part group's whole call measures the
-    same; DESIGN.md §4 "Blocking"); ``stats`` receives per-MPU PsMpuStats.
+    same; DESIGN.md §4 "Blocking"); ``stats`` receives per-MPU PsMpuStats, ``process_stats``
+    the reference's MPUSTATS (``lpProcessStats``, PS_Polygonizer.h:391).
     """
     if model.ct_prims == 0:
         return soa.RET_PARAM_ERROR, 0, poly_mpus
     if device not in _DEFAULT:
         _DEFAULT[device] = Polygonizer(device)
-    return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats)
+    return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats, process_stats)
 
 
 def _mesh_from_arrays(V, T, N, fill):

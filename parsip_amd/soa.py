@@ -97,11 +97,16 @@ MPU_DTYPE = np.dtype(
 )
 MPU_STATS_DTYPE = np.dtype([("passedPrecheck", "<u4"), ("ctFieldEvals", "<u4"),
                             ("ctVertices", "<u4"), ("ctTriangles", "<u4")])
+# MPUSTATS (PS_Polygonizer.h:201-207) in its LP64 layout (parsip_gpu.h PsMpuProcessStats):
+# tbb_thread::id = a pthread_t, tbb::tick_count = one long long (CLOCK_REALTIME ns)
+MPUSTATS_DTYPE = np.dtype([("idxThread", "<i4"), ("bIntersected", "<i4"), ("threadID", "<u8"),
+                           ("tickStart", "<i8"), ("tickEnd", "<i8")])
 
 assert PRIMS_DTYPE.itemsize == 9500
 assert PRIMS_DTYPE.fields["skeletType"][1] == 9216
 assert PRIMS_DTYPE.fields["ctPrims"][1] == 9496
 assert OPS_DTYPE.itemsize == 5636
+assert MPUSTATS_DTYPE.itemsize == 32 and MPUSTATS_DTYPE.fields["tickStart"][1] == 16
 assert OPS_DTYPE.fields["vBoxLoX"][1] == 512 and OPS_DTYPE.fields["resX"][1] == 3584
 assert PRIM_MATRICES_DTYPE.itemsize == 6148
 assert BOX_MATRICES_DTYPE.itemsize == 8196

@@ -8,6 +8,10 @@
 
 struct svec3f { float x, y, z; };
 struct PolyMPUs8 { PsMPU vMPUs[8]; uint32_t ctMPUs; };
+// a caller's MPUSTATS (PS_Polygonizer.h:201-207) with TBB-like opaque members
+class Tid { unsigned long id_ = 0; };
+class Tick { long long count_ = 0; };
+struct MPUSTATS { int idxThread; int bIntersected; Tid threadID; Tick tickStart; Tick tickEnd; };
 
 int main() {
     svec3f lo{-4, -4, -4}, hi{4, 4, 4};
@@ -32,5 +36,11 @@ int main() {
     std::printf("rc %d device %d\n", rc, (int)haveDevice);
     if (!haveDevice && rc != PSGPU_RET_DEVICE_ERROR) return 4;
     if (haveDevice && rc != PSGPU_RET_MPU_OVERFLOW) return 5;  // 2x2x2 lattice fits? see test
+    // the reference's optional lpProcessStats: NULL, nullptr and a caller MPUSTATS* all compile
+    static MPUSTATS stats[8];
+    const int r1 = psgpu::Polygonize(0.05f, prims, mats, ops, out, NULL);
+    const int r2 = psgpu::Polygonize(0.05f, prims, mats, ops, out, nullptr);
+    const int r3 = psgpu::Polygonize(0.05f, prims, mats, ops, out, stats);
+    if (r1 != rc || r2 != rc || r3 != rc) return 6;
     return 0;
 }

@@ -16,6 +16,13 @@
 //   soa <soa.bin> <cellsize> <polympus.bin>
 //        PS::SIMDPOLY::Polygonize on a PS::SIMDPOLY::PolyMPUs (24,000 MPUs, the reference's
 //        capacity); writes rc, ctMPUs and the MPUs.
+//   soa-stats <soa.bin> <cellsize> <stats.bin>
+//        the same with the reference's MPUSTATS* lpProcessStats: a caller-side MPUSTATS whose
+//        thread id and ticks are classes with private members, as legacy TBB's tbb_thread::id
+//        and tbb::tick_count; writes rc, ctMPUs, the host clock (CLOCK_REALTIME ns) before and
+//        after the call, then the ctMPUs 32-byte records.
+#include <time.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -103,6 +110,28 @@ void resolve_instances(std::vector<std::unique_ptr<CBlobNode>>& own) {
                     static_cast<CInstance*>(n.get())->origin = m.get();
                     break;
                 }
+}
+
+// The reference's MPUSTATS (PS_Polygonizer.h:201-207) over stand-ins with legacy TBB's
+// representations (tbb_thread::id: a pthread_t; tick_count: one long long).
+class ThreadIdLike {
+    unsigned long my_id = 0;
+};
+class TickCountLike {
+    long long my_count = 0;
+};
+struct MPUSTATS {
+    int idxThread;
+    int bIntersected;
+    ThreadIdLike threadID;
+    TickCountLike tickStart;
+    TickCountLike tickEnd;
+};
+
+long long now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec;
 }
 
 template <class T>
@@ -199,7 +228,7 @@ int main(int argc, char** argv) {
         o.write(reinterpret_cast<const char*>(tris.data()), (std::streamsize)(tris.size() * 4));
         return re == PSGPU_RET_SUCCESS ? 0 : 68;
     }
-    if (mode == "soa" && argc >= 5) {
+    if ((mode == "soa" || mode == "soa-stats") && argc >= 5) {
         static PS::SIMDPOLY::SOABlobPrims prims;
         static PS::SIMDPOLY::SOABlobPrimMatrices mats;
         static PS::SIMDPOLY::SOABlobOps ops;
@@ -212,7 +241,26 @@ int main(int argc, char** argv) {
         if (!in) return 65;
         std::unique_ptr<PS::SIMDPOLY::PolyMPUs> poly(new PS::SIMDPOLY::PolyMPUs());
         poly->ctMPUs = 12345;  // must be overwritten (0 on failure)
-        const int rc = PS::SIMDPOLY::Polygonize((float)std::atof(argv[3]), prims, mats, ops, *poly);
+        const float cs = (float)std::atof(argv[3]);
+        if (mode == "soa-stats") {
+            std::vector<MPUSTATS> stats(PSGPU_MAX_MPU_COUNT);
+            for (size_t i = 0; i < stats.size(); ++i) {  // fields the reference leaves alone
+                stats[i].idxThread = -7;
+                stats[i].bIntersected = (int)i;
+            }
+            const long long t0 = now_ns();
+            const int rc = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *poly, stats.data());
+            const long long t1 = now_ns();
+            std::printf("Polygonize rc %d ctMPUs %u\n", rc, poly->ctMPUs);
+            std::ofstream o(argv[4], std::ios::binary);
+            put(o, rc);
+            put(o, poly->ctMPUs);
+            put(o, t0);
+            put(o, t1);
+            o.write(reinterpret_cast<const char*>(stats.data()), (std::streamsize)poly->ctMPUs * sizeof(MPUSTATS));
+            return 0;
+        }
+        const int rc = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *poly, NULL);  // the reference's default
         std::printf("Polygonize rc %d ctMPUs %u\n", rc, poly->ctMPUs);
         std::ofstream o(argv[4], std::ios::binary);
         put(o, rc);
