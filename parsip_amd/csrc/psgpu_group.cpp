@@ -501,7 +501,8 @@ struct psgpu_comm {
     int nranks = 0, rank = 0, device = 0;
     uint32_t* gathered = nullptr;      // device: nranks x 8 words
     uint32_t* hostGathered = nullptr;  // pinned copy
-    uint32_t* flag = nullptr;          // device: the "some rank re-ran" all-reduce word
+    uint32_t* flag = nullptr;          // device: the "some rank re-ran" all-reduce word, then a
+                                       // constant 2 (a failed rank's contribution, no copy needed)
     uint32_t* hostFlag = nullptr;      // pinned
     bool pending = false;
     bool reexchanged = false;          // the last result needed the second exchange
@@ -540,9 +541,14 @@ int psgpu_comm_create(psgpu_ctx* ctx, const uint8_t id[PSGPU_COMM_ID_BYTES], int
     if (rc == PSGPU_RET_SUCCESS &&
         (hipMalloc(&m->gathered, (size_t)nranks * 8 * sizeof(uint32_t)) != hipSuccess ||
          hipHostMalloc(&m->hostGathered, (size_t)nranks * 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-         hipMalloc(&m->flag, sizeof(uint32_t)) != hipSuccess ||
+         hipMalloc(&m->flag, 2 * sizeof(uint32_t)) != hipSuccess ||
          hipHostMalloc(&m->hostFlag, 9 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess))
         rc = PSGPU_RET_DEVICE_ERROR;
+    if (rc == PSGPU_RET_SUCCESS) {
+        const uint32_t failWords[2] = {0u, 2u};
+        if (hipMemcpy(m->flag, failWords, sizeof(failWords), hipMemcpyHostToDevice) != hipSuccess)
+            rc = PSGPU_RET_DEVICE_ERROR;
+    }
     if (rc != PSGPU_RET_SUCCESS) {
         psgpu_comm_destroy(m);
         return rc;
@@ -565,7 +571,7 @@ void psgpu_comm_destroy(psgpu_comm* m) {
 // Enqueue the exchange of the context's last polygonization (its k_finish totals) on the
 // context's stream: ncclAllGather of 8 words per rank (psgpu_comm_result copies them to the host).
 int psgpu_comm_exchange(psgpu_comm* m, psgpu_ctx* ctx) {
-    if (!m || !ctx || ctx->device != m->device) return PSGPU_RET_PARAM_ERROR;
+    if (!m || !m->comm || !ctx || ctx->device != m->device) return PSGPU_RET_PARAM_ERROR;
     int rc = set_device(ctx);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     hipStream_t s = ctx->runStream ? ctx->runStream : ctx->stream;
@@ -581,7 +587,7 @@ int psgpu_comm_exchange(psgpu_comm* m, psgpu_ctx* ctx) {
 // streams): part 0's stream waits for the others' last launches, sums their totals and
 // all-gathers the sum.
 int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
-    if (!m || !g || g->parts.empty() || g->parts.size() > 16) return PSGPU_RET_PARAM_ERROR;
+    if (!m || !m->comm || !g || g->parts.empty() || g->parts.size() > 16) return PSGPU_RET_PARAM_ERROR;
     for (psgpu_ctx* c : g->parts)
         if (c->device != m->device) return PSGPU_RET_PARAM_ERROR;
     psgpu_ctx* c0 = g->parts[0];
@@ -624,14 +630,26 @@ int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
 // A rank whose finish fails still enters the all-reduce, with flag 2: then every rank
 // returns an error (its own, or PSGPU_RET_DEVICE_ERROR for another rank's failure) and
 // none waits for a collective the failed rank will not enter.
+// If even that cannot be prepared (the device cannot be made current, or the flag cannot be
+// copied to it), the rank still enters the all-reduce, from the constant 2 kept beside the flag
+// (no copy needed); should the collective itself fail to enqueue, the communicator is aborted
+// (ncclCommAbort) and unusable from then on -- psgpu_comm_destroy is all that is left to call.
 int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut) {
-    if (!m || !m->pending || !m->ctx) return PSGPU_RET_PARAM_ERROR;
+    if (!m || !m->pending || !m->ctx || !m->comm) return PSGPU_RET_PARAM_ERROR;
     psgpu_ctx* c = m->ctx;
     PsMeshInfo mine;
     int local = m->group ? psgpu_group_finish(m->group, &mine, nullptr) : psgpu_finish(c, &mine);
     m->pending = false;
-    if (hipSetDevice(m->device) != hipSuccess) return local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR;
     hipStream_t s = c->runStream ? c->runStream : c->stream;
+    auto enter_failed = [&](int rc) {  // this rank's flag 2, so that no other rank waits forever
+        if (ncclAllReduce(m->flag + 1, m->flag, 1, ncclUint32, ncclMax, m->comm, s) != ncclSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            (void)ncclCommAbort(m->comm);
+            m->comm = nullptr;
+        }
+        return rc;
+    };
+    if (hipSetDevice(m->device) != hipSuccess) return enter_failed(local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR);
     const size_t gb = (size_t)m->nranks * 8 * sizeof(uint32_t);
     uint32_t flag = 2u;
     if (local == PSGPU_RET_SUCCESS) {
@@ -657,7 +675,7 @@ int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut
     }
     *m->hostFlag = flag;
     if (hipMemcpyAsync(m->flag, m->hostFlag, sizeof(uint32_t), hipMemcpyHostToDevice, s) != hipSuccess)
-        return local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR;
+        return enter_failed(local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR);
     int rc = nccl_fail(ncclAllReduce(m->flag, m->flag, 1, ncclUint32, ncclMax, m->comm, s), "ncclAllReduce");
     if (rc != PSGPU_RET_SUCCESS) return local != PSGPU_RET_SUCCESS ? local : rc;
     PSGPU_CHECK(hipMemcpyAsync(m->hostFlag, m->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));

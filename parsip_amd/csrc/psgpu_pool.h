@@ -25,10 +25,19 @@ namespace psgpu {
 class ScatterPool {
 public:
     // `cpus`: where the workers may run (null: anywhere the process may)
+    // If a thread cannot be started, the ones already running are stopped and joined before
+    // the exception leaves (a destroyed joinable std::thread would terminate the process), so
+    // the caller's fallback (scatter on its own thread) can run.
     explicit ScatterPool(unsigned workers, const cpu_set_t* cpus = nullptr) {
-        for (unsigned i = 0; i < workers; ++i) {
-            th_.emplace_back([this] { work(); });
-            if (cpus) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof(cpu_set_t), cpus);
+        try {
+            th_.reserve(workers);
+            for (unsigned i = 0; i < workers; ++i) {
+                th_.emplace_back([this] { work(); });
+                if (cpus) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof(cpu_set_t), cpus);
+            }
+        } catch (...) {
+            stop_all();
+            throw;
         }
     }
     // The CPUs of the NUMA node the calling thread runs on, within the process's affinity set
@@ -67,14 +76,7 @@ public:
         *out = mine;
         return true;
     }
-    ~ScatterPool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (std::thread& t : th_) t.join();
-    }
+    ~ScatterPool() { stop_all(); }
     unsigned workers() const { return (unsigned)th_.size(); }
 
     // callerDrains: the calling thread takes tasks too (false: it only waits -- when the
@@ -95,6 +97,16 @@ public:
     }
 
 private:
+    void stop_all() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_)
+            if (t.joinable()) t.join();
+        th_.clear();
+    }
     void drain(uint32_t gen) {
         uint64_t v = state_.load(std::memory_order_acquire);
         for (;;) {
