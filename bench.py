@@ -291,34 +291,44 @@ def latency_single_parts(device, model, cs, jit, parts=2, reps=30):
         g.close()
 
 
-def blocking_contract(poly, config="C2", reps=10):
+def blocking_contract(polys, config="C2", reps=24):
     """The reference's own blocking contract, PCIe-inclusive: Polygonize into the caller's
     PolyMPUs (PS_Polygonizer.h:386-391 as SimdPoly::run calls it, PS_HighPerformanceRender.cpp:
     373-376): model upload, polygonization, mesh download and the scatter into the sparse
-    21.5-KB-per-MPU PolyMPUs layout.  `poly` is one context (gpu.Polygonizer: what
-    psgpu::Polygonize / gpu.Polygonize run on) or a gpu.Group of parts of the device.  C3
-    has 50,653 MPUs, past the reference's MAX_MPU_COUNT (24,000), so its PolyMPUs array is
-    allocated with room for them (1.09 GB).  Median over `reps` calls after 2 warm-ups."""
+    21.5-KB-per-MPU PolyMPUs layout.  `polys`: {name: engine}, each one context
+    (gpu.Polygonizer: what psgpu::Polygonize / gpu.Polygonize run on) or a gpu.Group of parts of
+    the device; their calls alternate, so every engine sees the same host and link conditions
+    (some boxes run a few calls in 24 several times slower: DESIGN.md §4 "Blocking").  C3 has
+    50,653 MPUs, past the reference's MAX_MPU_COUNT (24,000), so its PolyMPUs array is allocated
+    with room for them (1.09 GB).  Per engine: median, best and p90 over `reps` calls after 2
+    warm-ups."""
     from parsip_amd import soa
 
     model, cs, n = synth.make_config(config)
     ct_need = gpu.count_mpus(cs, *model.bbox)
     out = np.zeros(max(soa.MAX_MPU_COUNT, ct_need), soa.MPU_DTYPE)
     for _ in range(2):
-        rc, ct, _ = poly.polygonize_mpus(cs, model, out)
-        assert rc == 1 and ct == ct_need, (rc, ct)
-    t = []
+        for poly in polys.values():
+            rc, ct, _ = poly.polygonize_mpus(cs, model, out)
+            assert rc == 1 and ct == ct_need, (rc, ct)
+    t = {k: [] for k in polys}
     for _ in range(reps):
-        t0 = time.perf_counter()
-        poly.polygonize_mpus(cs, model, out)
-        t.append(time.perf_counter() - t0)
-    med = float(np.median(t))
-    engine = (f"psgpu_group_polygonize_mpus over {poly.n} parts of one device"
-              if isinstance(poly, gpu.Group) else "psgpu_polygonize_mpus on one context (the drop-ins' default)")
-    return {"config": f"{config}: {model.ct_prims}-prim BlobTree, {n}^3 cells, {ct} MPUs", "ms": round(med * 1e3, 3),
-            "best_ms": round(min(t) * 1e3, 3), "mcells_per_s": round(n ** 3 / med / 1e6, 2), "engine": engine,
-            "note": "end to end (SoA upload, the kernel chains, compact-mesh download over PCIe, host scatter into "
-                    "PolyMPUs); never the bench value"}
+        for k, poly in polys.items():
+            t0 = time.perf_counter()
+            poly.polygonize_mpus(cs, model, out)
+            t[k].append(time.perf_counter() - t0)
+    res = {}
+    for k, poly in polys.items():
+        med = float(np.median(t[k]))
+        engine = (f"psgpu_group_polygonize_mpus over {poly.n} parts of one device"
+                  if isinstance(poly, gpu.Group) else "psgpu_polygonize_mpus on one context (the drop-ins' default)")
+        res[k] = {"config": f"{config}: {model.ct_prims}-prim BlobTree, {n}^3 cells, {ct_need} MPUs",
+                  "ms": round(med * 1e3, 3), "best_ms": round(min(t[k]) * 1e3, 3),
+                  "p90_ms": round(float(np.percentile(t[k], 90)) * 1e3, 3), "calls": reps,
+                  "mcells_per_s": round(n ** 3 / med / 1e6, 2), "engine": engine,
+                  "note": "end to end (SoA upload, the kernel chains, compact-mesh download over PCIe, host scatter "
+                          "into PolyMPUs); never the bench value"}
+    return res
 
 
 class Engine:
@@ -890,14 +900,15 @@ def main():
         # the drop-ins' blocking contract (psgpu::Polygonize / gpu.Polygonize: one context), C2
         # and the headline's C3; beside it C3 on a 2-part group of the device (shorter kernels,
         # the same whole call: DESIGN.md §4 "Blocking")
-        out["blocking_polygonize_mpus"] = blocking_contract(poly, "C2")
-        out["blocking_polygonize_mpus_c3"] = blocking_contract(poly, "C3")
+        out["blocking_polygonize_mpus"] = blocking_contract({"one": poly}, "C2")["one"]
         bg = gpu.Group([device, device])
         try:
             bg.set_option(gpu.GROUP_OPT_BALANCE, gpu.BALANCE_PLAN)
             bg.set_option(gpu.GROUP_OPT_MIN_PART_MPUS, gpu.BLOCKING_MIN_PART_MPUS)
             bg.set_option(gpu.OPT_JIT, args.jit)
-            out["blocking_polygonize_mpus_c3_2parts"] = blocking_contract(bg, "C3")
+            b3 = blocking_contract({"one": poly, "2parts": bg}, "C3")  # calls alternate
+            out["blocking_polygonize_mpus_c3"] = b3["one"]
+            out["blocking_polygonize_mpus_c3_2parts"] = b3["2parts"]
         finally:
             bg.close()
     if grp.rank == 0 and grp.world == 1 and not args.no_cpu:

@@ -133,8 +133,8 @@ typedef struct PsMPU {                   /* MPU, PS_Polygonizer.h:183-195 */
     uint32_t ctFieldEvals;
 } PsMPU;
 
-/* Per-MPU statistics (replaces MPUSTATS, PS_Polygonizer.h:201-207: GPU work has no
- * thread id / tick pair, so the export is the per-MPU outcome instead). */
+/* Per-MPU outcome of a run (the library's own record; the reference's MPUSTATS is
+ * PsMpuProcessStats below -- a different layout). */
 typedef struct PsMpuStats {
     uint32_t passedPrecheck;   /* S1 (8-corner F>0 test) passed                  */
     uint32_t ctFieldEvals;     /* 128 if S1 passed else 0 (reference counter)     */
@@ -336,8 +336,8 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        specialised kernels on a host thread while the interpreter
                                        serves polygonizations (bit-identical output); 0: block */
 /* Host-only (no GPU): compile the model's specialised kernels with hiprtc (mode 1:
- * structure only, 2: parameters baked in); returns the code-object size or a negative
- * error (log receives the compiler output). */
+ * structure only, 2: parameters baked in; | 4: with the tree-split kernels); returns the
+ * code-object size or a negative error (log receives the compiler output). */
 long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* matrices,
                        const PsSoaBlobOps* ops, int mode, char* log, size_t cap);
 /* 1 if the current model runs on run-time specialised kernels, 0 on the interpreter. */

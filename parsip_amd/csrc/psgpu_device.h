@@ -726,6 +726,20 @@ __device__ __forceinline__ void phase_stamp(const Params& p, int ph, uint32_t bi
     const uint64_t t = stamp_now();
     if (lane_id() == 0) p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)w + ph] = t;
 }
+// The same, taken only once `dep` has been computed (inline asm keeps the clock read after its
+// producer and in program order with the other stamps): phases of k_finish (debug bit 2048;
+// the stamps change the kernel's registers, so they exist only when PSGPU_FIN_PHASES is 1).
+#ifndef PSGPU_FIN_PHASES
+#define PSGPU_FIN_PHASES 0  // compiled in only for the measurement (PSGPU_JIT_FLAGS=-DPSGPU_FIN_PHASES=1)
+#endif
+__device__ __forceinline__ void phase_stamp_after(const Params& p, int ph, uint32_t bit, float dep) {
+    if (!PSGPU_FIN_PHASES || !(p.debug & bit) || !p.stamps) return;
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= p.stampCap) return;
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep));
+    if (lane_id() == 0) p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)w + ph] = t;
+}
 // A kernel's span in one run (PSGPU_OPT_SPANS): every wave folds its start / end into one of
 // 64 {min start, max end} pairs of the run's slot (chosen by block, so no address sees more
 // than 1/64 of the waves' atomics); the host reduces the 64 pairs to the first wave start and
@@ -1677,6 +1691,42 @@ if constexpr (VPW == 64) {
 }
 }
 
+#ifndef PSGPU_FIN_TRI_PREFETCH
+#define PSGPU_FIN_TRI_PREFETCH 0  // measured neutral (isolated k_finish 27.8 us either way, r05)
+#endif
+// One lane's triangle record of a k_finish batch and its MPU's (V | T << 32) offset: the
+// global triangle gt = T offset + local id, its corners = V offset + local vertex ids (S6,
+// PS_Polygonizer.cpp:816-825, in the compact mesh's MPU order).
+struct TriPre {
+    TriRec R;
+    uint64_t o;
+    bool ok;
+};
+__device__ __forceinline__ TriPre tri_load(const Params& p, const ShardBatches& sb, uint32_t batch) {
+    TriPre t;
+    t.ok = false;
+    t.R = TriRec{0u, 0u};
+    t.o = 0ull;
+    if (batch >= sb.total) return t;
+    uint32_t shard, first, count;
+    sb.locate(batch, &shard, &first, &count);
+    const uint32_t i = first + lane_id();
+    if (i >= count) return t;
+    t.R = p.tq[(size_t)shard * p.tShardCap + i];
+    t.o = p.offs[((t.R.a >> 12) << 6) | shard];  // the record's shard is w & 63
+    t.ok = true;
+    return t;
+}
+__device__ __forceinline__ void tri_store(const Params& p, const TriPre& t) {
+    if (!t.ok) return;
+    const uint32_t gt = (uint32_t)(t.o >> 32) + (t.R.a & 2047u);
+    const uint32_t base = (uint32_t)t.o;
+    if (gt >= p.tCap) return;  // finish() grows and re-runs
+    p.tris[gt * 3 + 0] = base + (t.R.b & 2047u);
+    p.tris[gt * 3 + 1] = base + ((t.R.b >> 11) & 2047u);
+    p.tris[gt * 3 + 2] = base + ((t.R.b >> 22) | (((t.R.a >> 11) & 1u) << 10));
+}
+
 // Finish: per vertex fieldValueAndColor's value and colour walk (PS_Polygonizer.cpp:777-778,
 // 1378-1551) and the three normal samples (:780-781, 1598-1622), then the triangle records
 // -> global vertex ids.  Runs after k_vertex wrote the roots.  VPW 64: one lane per
@@ -1693,6 +1743,7 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
     const float delta = 0.001f;
     const float inv = -1.0f / delta;
+    phase_stamp_after(p, 0, 2048u, 0.0f);
     if (blockIdx.x == 0) {  // the run's counters for the host (mapped pinned memory)
         const uint32_t* src = reinterpret_cast<const uint32_t*>(p.ctr);
         uint32_t* dst = reinterpret_cast<uint32_t*>(p.hostCtr);
@@ -1717,6 +1768,13 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
     stage_shard_counts(p, 1, sCnt);            // ShardCtr::v
     stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
     __syncthreads();
+#if PSGPU_FIN_TRI_PREFETCH
+    // the wave's first triangle batch loaded before the vertex walk: its records and their
+    // MPUs' offsets do not depend on the walk, so their two dependent loads overlap it
+    const ShardBatches sbp(sCnt + kShards, p.tShardCap, 64);
+    const TriPre tp0 = tri_load(p, sbp, wave0);
+#endif
+    phase_stamp_after(p, 1, 2048u, 0.0f);
 if constexpr (VPW == 16) {
     // a quad of lanes per vertex: lane j of the quad walks point j (p, p + delta e_x,
     // p + delta e_y, p + delta e_z) with the same per-point pruning (GROUP 1) as the
@@ -1852,6 +1910,7 @@ if constexpr (VPW == 16) {
         const bool onSeg = R.scale >= 0.0f && R.scale <= 1.0f;
         float c[3] = {0.0f, 0.0f, 0.0f};
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        phase_stamp_after(p, 2, 2048u, P[0] + P[1] + P[2]);  // records in, root recomputed
         if (!(p.debug & 32u)) {  // ablation bit 5: no walks
             // vertices on their segments: the MPU masks (boxes grown by delta) cover p and
             // every normal sample; otherwise the wave's own box grown by delta
@@ -1860,6 +1919,7 @@ if constexpr (VPW == 16) {
                 if (ballot(!onSeg) == 0ull) cm = cull_mask_mpus(p, K.w);
                 else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
             }
+            phase_stamp_after(p, 3, 2048u, __uint_as_float((uint32_t)(cm.lo ^ cm.hi)));
             // value + colour at p and the normal's per-point fieldValue at p + delta*e_a
             // (:1598-1622) as four points of one walk (the colour of points 1-3 is dead
             // code); then SimdNormalize (rsqrt -> IEEE 1/sqrtf)
@@ -1868,6 +1928,7 @@ if constexpr (VPW == 16) {
             const float qz[4] = {P[2], P[2], P[2], P[2] + delta};
             float g[4], c4[12];
             ev.template evaln<1, true, 4>(qx, qy, qz, cm, g, c4);
+            phase_stamp_after(p, 4, 2048u, g[0] + g[1] + g[2] + g[3] + c4[0] + c4[1] + c4[2]);
             c[0] = c4[0];
             c[1] = c4[1];
             c[2] = c4[2];
@@ -1891,11 +1952,17 @@ if constexpr (VPW == 16) {
             p.col[gi * 3 + 1] = c[1];
             p.col[gi * 3 + 2] = c[2];
         }
+        phase_stamp_after(p, 5, 2048u, __uint_as_float(gi));
     }
 }
     if (p.debug & 64u) return;  // ablation bit 6: no triangles
     const ShardBatches sb(sCnt + kShards, p.tShardCap, 64);
-    for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
+    uint32_t batch0 = wave0;
+#if PSGPU_FIN_TRI_PREFETCH
+    tri_store(p, tp0);
+    batch0 += nWaves;
+#endif
+    for (uint32_t batch = batch0; batch < sb.total; batch += nWaves) {
         uint32_t shard, first, count;
         sb.locate(batch, &shard, &first, &count);
         const uint32_t t = first + lane;
@@ -1909,6 +1976,7 @@ if constexpr (VPW == 16) {
         p.tris[gt * 3 + 1] = base + ((R.b >> 11) & 2047u);
         p.tris[gt * 3 + 2] = base + ((R.b >> 22) | (((R.a >> 11) & 1u) << 10));
     }
+    phase_stamp_after(p, 6, 2048u, 0.0f);
 }
 
 // Field probe for tests: mode 0 quads of consecutive points, 1 per point, 2 + colour.

@@ -490,7 +490,8 @@ Params make_params(psgpu_ctx* c) {
     // k_mpu: one wave per queued survivor, as many as the last finished run queued + 1/4
     // (a run that queues more is re-run by finish(): the grid then fits exactly)
     const uint32_t maxBlocks = (c->mpuCount + mpb - 1) / mpb;
-    const uint32_t want = c->haveQueued ? (c->lastQueued + c->lastQueued / 4 + 256 + mpb - 1) / mpb : maxBlocks;
+    const uint32_t margin = c->lastQueued / c->mpuMarginDiv + (c->mpuMarginDiv > 4 ? 64u : 256u);
+    const uint32_t want = c->haveQueued ? (c->lastQueued + margin + mpb - 1) / mpb : maxBlocks;
     p.mpuBlocks = std::max(1u, std::min(maxBlocks, want));
     if (c->debug & (1 << 20)) p.mpuBlocks = 1;  // test hook: a k_mpu grid that falls short (finish re-runs)
     p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
@@ -580,12 +581,21 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
-    const uint32_t gridV = std::max(persistV, p.scanBlocks);
-    if (J) PSGPU_CHECK(launch_jit(vertex_vpw(c) == 64 ? J->vertexW : J->vertex, gridV, 256, 0, s, p));
+    const int vpwV = J ? vertex_vpw(c) : 16;
+    uint32_t gridV = std::max(persistV, p.scanBlocks);
+    uint32_t gridF = persistF;
+    if (c->gridFit && c->lastV) {
+        // grids fitted to the last finished run: a wave per batch of its vertices + 1/8 (both
+        // kernels stride over any rest), not the persistent grids' mostly empty waves
+        const uint64_t vv = (uint64_t)c->lastV + c->lastV / 8 + 256;
+        gridV = std::max(p.scanBlocks, std::min<uint32_t>(gridV, (uint32_t)((vv + 4ull * vpwV - 1) / (4ull * vpwV))));
+        gridF = std::min<uint32_t>(gridF, (uint32_t)((vv + 4ull * vpw - 1) / (4ull * vpw)));
+    }
+    if (J) PSGPU_CHECK(launch_jit(vpwV == 64 ? J->vertexW : J->vertex, gridV, 256, 0, s, p));
     else PSGPU_CHECK(launch_vertex(p, s, gridV));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[3], s));
-    if (J) PSGPU_CHECK(launch_jit(vpw == 16 ? J->finishQ : (vpw == 32 ? J->finishP : J->finish), persistF, 256, 0, s, p));
-    else PSGPU_CHECK(launch_finish(p, s, persistF, vpw));
+    if (J) PSGPU_CHECK(launch_jit(vpw == 16 ? J->finishQ : (vpw == 32 ? J->finishP : J->finish), gridF, 256, 0, s, p));
+    else PSGPU_CHECK(launch_finish(p, s, gridF, vpw));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[4], s));
     return PSGPU_RET_SUCCESS;
 }
@@ -975,6 +985,10 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (jitEnv) c->useJit = std::min(3, std::max(0, atoi(jitEnv)));
     const char* asyncEnv = getenv("PSGPU_JIT_ASYNC");
     if (asyncEnv) c->jitAsync = atoi(asyncEnv) != 0;
+    if (const char* e = getenv("PSGPU_GRID_FIT")) c->gridFit = atoi(e) != 0;          // A/B tooling
+    if (const char* e = getenv("PSGPU_FINISH_QUAD")) c->finishQuad = std::min(3, std::max(0, atoi(e)));
+    if (const char* e = getenv("PSGPU_VERTEX_WIDE")) c->vertexWide = std::min(2, std::max(0, atoi(e)));
+    if (const char* e = getenv("PSGPU_MPU_MARGIN")) c->mpuMarginDiv = std::max(1, atoi(e));
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -1809,7 +1823,7 @@ long psgpu_jit_compile(const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mat
     int rc = build_device_model(*prims, *mats, *ops, *m);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     std::string err;
-    long n = jit_compile_only(*m, mode == 2, &err);
+    long n = jit_compile_only(*m, (mode & 3) == 2, &err, (mode & 4) != 0);
     if (log && cap) {
         const size_t k = std::min(cap - 1, err.size());
         memcpy(log, err.data(), k);

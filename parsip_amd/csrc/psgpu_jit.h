@@ -36,7 +36,7 @@ JitFuture jit_request(const DevModel& m, bool baked, bool useDisk = true, bool s
 // per device; nullptr + *err on failure (a stale cached object is dropped from the cache).
 std::shared_ptr<JitKernels> jit_load(const JitCode& code, int device, std::string* err);
 // Compile (and cache) without loading: code-object size, or -1 and *err.  No GPU needed.
-long jit_compile_only(const DevModel& m, bool baked, std::string* err);
+long jit_compile_only(const DevModel& m, bool baked, std::string* err, bool split = false);
 // The generated HIP source (tests and debugging).
 std::string jit_source(const DevModel& m, bool baked, bool split = false);
 // the generated walk splits at the root (TreeEval::kSplit): a binary known op over two ops

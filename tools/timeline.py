@@ -179,7 +179,55 @@ def precheck_phases(config="C3", share=1):
                   + f" | end {(rec[w, 1] - ph[w, 3]) * TICK_US if ph[w, 3] else -1:.2f}")
 
 
+def finish_phases(config="C3", share=1):
+    """k_finish phase stamps of the 64-vertex layout (debug bit 2048; the kernels must be
+    compiled with PSGPU_JIT_FLAGS=-DPSGPU_FIN_PHASES=1): per wave with a batch, entry ->
+    counts staged (block barrier) -> records loaded and root recomputed -> culling mask ->
+    the 4-point colour walk -> vertex stores issued -> triangle pass -> the record's end."""
+    model, cs, N = synth.make_config(config)
+    p = gpu.Polygonizer(0)
+    p.set_option(gpu.OPT_FINISH_QUAD, 0)
+    p.set_model(model)
+    lo, hi = _share_range(p, cs, share)
+    for _ in range(3):
+        p.run(cs, lo, hi)
+    p.set_option(gpu.OPT_STAMPS, 1 << 16)
+    p.set_option(gpu.OPT_DEBUG, 2048)
+    p.run(cs, lo, hi)
+    S = p.stamps()
+    rec = S["k_finish"].astype(np.int64)
+    n = len(rec)
+    ph = S["mpu_phases"].astype(np.int64)[:n]
+    real = ph[:, 4] != 0
+    t0 = rec[:, 0].min()
+    print(f"k_finish waves {n}, with a vertex batch {int(real.sum())}; span "
+          f"{(rec[:, 1].max() - t0) * TICK_US:.2f} us")
+    names = ["entry->staged", "staged->root", "root->cullmask", "walk", "stores", "triangles", "->end"]
+    cols = [ph[:, 0], ph[:, 1], ph[:, 2], ph[:, 3], ph[:, 4], ph[:, 5], ph[:, 6], rec[:, 1]]
+    for i, nm in enumerate(names):
+        a, b = cols[i][real], cols[i + 1][real]
+        ok = (a > 0) & (b > 0)
+        dt = (b[ok] - a[ok]) * TICK_US
+        if len(dt):
+            print(f"  {nm:15s} median {np.median(dt):6.2f} us  p90 {np.percentile(dt, 90):6.2f}  max {dt.max():6.2f}")
+    life = (rec[real, 1] - rec[real, 0]) * TICK_US
+    st = (rec[real, 0] - t0) * TICK_US
+    print(f"  life median {np.median(life):.2f} p90 {np.percentile(life, 90):.2f} max {life.max():.2f}; "
+          f"start median {np.median(st):.2f} max {st.max():.2f}")
+    # the waves that end last: what they spent their time on
+    worst = np.argsort(rec[:, 1])[-8:]
+    for w in worst:
+        if not real[w]:
+            continue
+        seg = [(cols[i + 1][w] - cols[i][w]) * TICK_US for i in range(len(names))]
+        print(f"  late wave {w}: start {(rec[w, 0] - t0) * TICK_US:.2f} end {(rec[w, 1] - t0) * TICK_US:.2f} | "
+              + " ".join(f"{x:.2f}" for x in seg))
+
+
 if __name__ == "__main__":
+    if "--finish" in sys.argv:
+        finish_phases(share=int(os.environ.get("SHARE", "1")))
+        sys.exit(0)
     share = int(os.environ.get("SHARE", "1"))
     if "--precheck" in sys.argv:
         sys.argv.remove("--precheck")
