@@ -77,6 +77,10 @@ __device__ __forceinline__ bool quad_any(bool v) {
                           // in flight 0.0611-0.0624 vs 0.0555-0.0560 ms/step (r04 A/B,
                           // profiles/r04_kernel_variants_ab.txt): kept as an experiment
 #endif
+#ifndef PSGPU_S2_OCT
+#define PSGPU_S2_OCT 0  // S2 by octant passes (k_precheck's per-octant proofs): 0 off, 1 when <= 4
+                        // octants are unproven, 2 always (two passes when 5-8 are unproven)
+#endif
 constexpr int kS2Group = PSGPU_S2_GROUP;
 template <int GROUP>
 __device__ __forceinline__ bool group_any(bool v) {
@@ -893,6 +897,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     // the 4x4x4 corners [4X, 4X+3] x [4Y, 4Y+3] x [4Z, 4Z+3] of its S2 cache (its z range
     // is exactly one S2 quad); the wave's culling box covers every MPU of the brick.
     uint32_t proven8 = 0;
+    uint64_t octOut = 0ull, octIn = 0ull;  // per lane (MPU g, octant c): proven all outside / all inside
     if ((p.debug & 1024u) && flags8 != 0u) __builtin_amdgcn_s_setprio(2);  // experiment: heavy waves first
     if constexpr (SPLIT == 2) {
         __shared__ float sLo[4][64], sHi[4][64];
@@ -926,6 +931,8 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
             ok = sOk[r][lane] != 0u && sOk[l][lane] != 0u;
             ev.bound_combine(sLo[r][lane], sHi[r][lane], sLo[l][lane], sHi[l][lane], cm, &lo, &hi);
             const uint64_t bOut = ballot(ok && hi < 0.5f), bIn = ballot(ok && lo >= 0.5f);
+            octOut = bOut;
+            octIn = bIn;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const bool all = ((bOut >> (8 * q)) & 0xffull) == 0xffull || ((bIn >> (8 * q)) & 0xffull) == 0xffull;
@@ -950,6 +957,8 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
         bool ok = true;
         ev.bound(B, cm, &lo, &hi, &ok);
         const uint64_t bOut = ballot(ok && hi < 0.5f), bIn = ballot(ok && lo >= 0.5f);
+        octOut = bOut;
+        octIn = bIn;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const bool all = ((bOut >> (8 * q)) & 0xffull) == 0xffull || ((bIn >> (8 * q)) & 0xffull) == 0xffull;
@@ -976,7 +985,14 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(queue8));
     base = lane_value(base, 0);
-    if (pass) p.pq[shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u))] = mOf;
+    if (pass) {
+        const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
+        p.pq[slotq] = mOf;
+        // the MPU's octants proven uniform by the same bounds: k_mpu evaluates only the others
+        // (their inside bits are the proof's), bits 0-7 all outside, 8-15 all inside
+        if (PSGPU_S2_OCT)
+            p.pqOct[slotq] = (uint16_t)(((octOut >> (8 * lane)) & 0xffull) | (((octIn >> (8 * lane)) & 0xffull) << 8));
+    }
     phase_stamp(p, 3, 8192u);
     // Culling mask of each queued MPU, from this wave's culling segments (already in
     // registers): its box grown by the normal delta, for k_vertex / k_finish (mpuMasks) and,
@@ -1046,6 +1062,84 @@ __device__ __forceinline__ void mpu_sync() {
     }
 }
 
+// S2 over the octants k_precheck could not prove uniform (bounds of the 4x4x4 corners
+// [4X, 4X+3] x [4Y, 4Y+3] x [4Z, 4Z+3], exactly the corner coordinates below): a pass walks up
+// to 4 octants, 16 lanes each -- lane (slot, yy, zz), a 4-point x-needle per lane -- so every
+// 4-lane pruning group is 4 z-consecutive corners z = 4Z..4Z+3 of one x and y, the
+// reference's S2 quads (:550-610), and every corner's value is the one the 8x8x8 walk gives.
+// Proven octants contribute their proof's inside bits.  ins[x] bit y*8 + z, as the 8-needle
+// layout's ballots; returned by lane 0 into sIns.
+template <int GROUP, class EV>
+__device__ __forceinline__ void s2_octants(const EV& ev, const float o[3], float cs, const CullMask& cm, uint32_t oct,
+                                           uint32_t U, int lane, uint64_t* sIns) {
+    uint64_t ins[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) ins[x] = 0ull;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if ((oct >> (8 + c)) & 1u) {  // octant c = X | Y << 1 | Z << 2 proven all inside
+            const uint64_t m = 0x0F0F0F0Full << (32 * ((c >> 1) & 1) + 4 * (c >> 2));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (c & 1) ins[4 + i] |= m;
+                else ins[i] |= m;
+            }
+        }
+    }
+    const int sl = lane >> 4, yy = (lane >> 2) & 3, zz = lane & 3;
+    uint32_t rest = U;
+#pragma unroll 1
+    while (rest != 0u) {
+        const uint32_t cur = rest;
+        // this lane's octant: the sl-th set bit of cur (a lane past the pass's octants repeats
+        // the first; its values are not used)
+        uint32_t cl = cur;
+        for (int j = 0; j < sl; ++j)
+            if (cl & (cl - 1u)) cl &= cl - 1u;
+            else cl = cur;
+        if (sl >= __popc(cur)) cl = cur;
+        const int c = __builtin_ctz(cl);
+        const int X = c & 1, Y = (c >> 1) & 1, Z = c >> 2;
+        float px[4], py[4], pz[4], f[4];
+        const float yv = o[1] + (float)(4 * Y + yy) * cs;
+        const float zv = o[2] + (float)(4 * Z + zz) * cs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            px[i] = o[0] + (float)(4 * X + i) * cs;
+            py[i] = yv;
+            pz[i] = zv;
+        }
+        ev.template evaln<GROUP, false, 4>(px, py, pz, cm, f, nullptr);
+        uint32_t slots = cur;  // the pass's octants in slot order
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t b = ballot(f[i] >= 0.5f);
+            uint32_t sc = slots;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (sc == 0u) break;
+                const int cs_ = __builtin_ctz(sc);
+                sc &= sc - 1u;
+                const uint32_t bits = (uint32_t)(b >> (16 * s)) & 0xffffu;
+                const int Ys = (cs_ >> 1) & 1, Zs = cs_ >> 2;
+                uint64_t v = 0ull;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v |= (uint64_t)((bits >> (4 * r)) & 0xfu) << ((4 * Ys + r) * 8 + 4 * Zs);
+                if (cs_ & 1) ins[4 + i] |= v;
+                else ins[i] |= v;
+            }
+        }
+        // drop the pass's (up to) 4 octants
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (rest) rest &= rest - 1u;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int x = 0; x < 8; ++x) sIns[x] = ins[x];
+    }
+}
+
 // Per-MPU body: W = kMpuWaves wavefronts per MPU that passed S1 (and was not proven
 // empty), 4 wavefronts per block.  Every wave of a block reaches every barrier: waves
 // without an MPU (past the last survivor) or whose MPU has no surface just skip the work.
@@ -1087,6 +1181,8 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     uint32_t m = 0, w = 0;
     float o[3] = {0.0f, 0.0f, 0.0f};
     CullMask cm{0ull, 0ull};
+    uint32_t oct = 0;  // k_precheck's octant proofs (PSGPU_S2_OCT)
+    (void)oct;
     if (live) {
         const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
         const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
@@ -1102,6 +1198,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
             cm.hi = p.pqMask[2 * slotq + 1];
 #endif
         }
+        if (PSGPU_S2_OCT) oct = uniform((uint32_t)p.pqOct[slotq]);
         *item = m;
         w = m - p.mpuBegin;  // slot of the MPU in the range: counts / offsets index
         mpu_origin(p, m, o);
@@ -1137,6 +1234,14 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
             if (part == 0) ev.template evaln_part<kS2Group, false, 8, 0>(pxs, pys, pzs, cm, fs, nullptr);
             else ev.template evaln_part<kS2Group, false, 8, 1>(pxs, pys, pzs, cm, fs, nullptr);
         } else {
+#if PSGPU_S2_OCT
+        const uint32_t U = ~(oct | (oct >> 8)) & 0xffu;  // octants without a proof
+        if (WPM == 1 && (PSGPU_S2_OCT == 2 || __popc(U) <= 4)) {
+            s2_octants<kS2Group>(ev, o, cs, cm, oct, U, lane, sIns);
+        } else {
+#else
+        {
+#endif
 #if PSGPU_S2_N == 1
         // one walk per x-slice in a runtime loop: the walk's code stays resident in the
         // instruction cache (unrolled copies of a 32-primitive walk do not fit)
@@ -1152,6 +1257,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         for (int x = 0; x < NX; ++x) {
             const uint64_t b = ballot(fs[x] >= 0.5f);
             if (lane == 0) sIns[part * NX + x] = b;
+        }
         }
         }
     }

@@ -439,6 +439,7 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
     PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->pqMask, c->capPqMask, (size_t)c->pShardCap * kShards * 2));
+    PSGPU_CHECK(grow(c->pqOct, c->capPqOct, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
     PSGPU_CHECK(grow(c->passed, c->capPassed, n));
     PSGPU_CHECK(grow(c->mpuMasks, c->capMasks, 2 * n));
@@ -486,6 +487,7 @@ Params make_params(psgpu_ctx* c) {
     p.brickStride = brick_stride((uint32_t)brick_count(c), (c->debug & 16384) != 0);
     p.pq = c->pq;
     p.pqMask = c->pqMask;
+    p.pqOct = c->pqOct;
     p.pShardCap = c->pShardCap;
     // k_mpu: one wave per queued survivor, as many as the last finished run queued + 1/4
     // (a run that queues more is re-run by finish(): the grid then fits exactly)
@@ -1009,7 +1011,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     c->tier2Fut = JitFuture();
     c->jit.reset();
     c->jit1.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->pqOct, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans, c->mpuTicks};
     for (void* b : bufs)
         if (b) (void)hipFree(b);

@@ -88,6 +88,8 @@ struct psgpu_ctx {
     size_t capLb = 0, capList = 0, capCounts = 0, capOff = 0, capVk = 0, capVp = 0, capTq = 0, capV = 0, capT = 0;
     uint32_t* pq = nullptr;         // sharded S1 survivor queues
     uint64_t* pqMask = nullptr;     // 2 words per queue entry (culling mask of the MPU box)
+    uint16_t* pqOct = nullptr;      // per queue entry: octant proofs (Params::pqOct)
+    size_t capPqOct = 0;
     size_t capPqMask = 0;
     uint32_t pShardCap = 0;
     uint32_t lastQueued = 0;        // S1 survivors queued for S2 in the last finished run

@@ -214,6 +214,7 @@ struct Params {
                             // permutation that spreads the surface's heavy bricks over the CUs)
     uint32_t* pq;           // kShards queues of pShardCap S1 survivors (global MPU ids)
     uint64_t* pqMask;       // per queue entry: the MPU box's culling mask (2 words, by k_precheck)
+    uint16_t* pqOct;        // per queue entry: octants proven all outside (bits 0-7) / inside (8-15)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
     uint32_t mpuBlocks;     // k_mpu grid (4 waves per block, kMpusPerBlock queued survivors per block)
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
