@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--engines", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--config", default="C3")
+    ap.add_argument("--stagger-us", type=float, default=0.0, help="the first round's engines start this far apart")
     a = ap.parse_args()
     model, cs, N = synth.make_config(a.config)
     E = a.engines
@@ -50,6 +51,10 @@ def main():
         t0 = time.perf_counter()
         for k in range(a.steps):
             eng[k % E].polygonize(cs)
+            if k < E - 1 and a.stagger_us > 0:
+                ts = time.perf_counter() + a.stagger_us * 1e-6
+                while time.perf_counter() < ts:
+                    pass
         t_enq = time.perf_counter()
         for e in eng:
             e.finish()
