@@ -1038,7 +1038,11 @@ constexpr int kLdsIns = ((kLdsTbase + 344 * 2) + 7) & ~7;
 constexpr int kLdsQ = kLdsIns + 8 * 8;
 constexpr int kLdsMpu = ((kLdsQ + 8) + 15) & ~15;
 constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
-constexpr int kLdsWaveSlots = kMpusPerBlock * kLdsMpu;  // interpreter slots follow
+#ifndef PSGPU_MPU_LDS_TABLES
+#define PSGPU_MPU_LDS_TABLES 1  // k_mpu gathers its MC table words from an LDS copy (A/B knob)
+#endif
+constexpr int kLdsTabOff = kMpusPerBlock * kLdsMpu;  // the block's copy of the tables
+constexpr int kLdsWaveSlots = kLdsTabOff + (PSGPU_MPU_LDS_TABLES ? kLdsTables : 0);  // interpreter slots follow
 
 // Last cell c in [0, 343) with first[c] <= r (first[] = exclusive prefix of per-cell
 // counts, non-decreasing, first[0] = 0, so that cell holds item r): binary lifting,
@@ -1165,7 +1169,21 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     phase_stamp(p, 0);
     const uint32_t d = blockIdx.x * (uint32_t)MPB + (uint32_t)slot;
     ModelPtr M = as_const(p.model);
+#if PSGPU_MPU_LDS_TABLES
+    // the MC tables passes 1-3 gather from (5.9 KB) copied into the block's LDS while wave 0
+    // reads the shard counts, one barrier for both: each gather then costs an LDS round trip
+    // (~50 cycles) instead of an L1 / L2 one (~200; MI355X_MICROARCH.md).  Not in the tree-split
+    // kernel, whose own LDS already limits it to 5 blocks per CU (it is launched without room)
     const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
+    if constexpr (SPLIT == 1) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.tables);
+        uint4* dst = reinterpret_cast<uint4*>(smem + kLdsTabOff);
+        for (int i = (int)threadIdx.x; i < kLdsTables / 16; i += (int)blockDim.x) dst[i] = src[i];
+        tab = reinterpret_cast<const CubeTablesDev*>(smem + kLdsTabOff);
+    }
+#else
+    const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
+#endif
     // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
     // the block
     __shared__ uint32_t sIncl[kShards];
