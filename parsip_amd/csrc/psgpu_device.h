@@ -1019,9 +1019,6 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     }
 }
 
-#ifndef PSGPU_PASS1_HOIST
-#define PSGPU_PASS1_HOIST 1  // k_mpu pass 1: the 7 slabs' table words loaded together (A/B knob)
-#endif
 #ifndef PSGPU_S2_N
 #define PSGPU_S2_N (8 / PSGPU_MPU_WAVES)  // x-slices per walk: one walk per (y,z) needle shares each
                                           // primitive's uniform work and (y,z) terms over its points
@@ -1038,11 +1035,7 @@ constexpr int kLdsIns = ((kLdsTbase + 344 * 2) + 7) & ~7;
 constexpr int kLdsQ = kLdsIns + 8 * 8;
 constexpr int kLdsMpu = ((kLdsQ + 8) + 15) & ~15;
 constexpr int kLdsTables = (int)((sizeof(CubeTablesDev) + 15) & ~(size_t)15);
-#ifndef PSGPU_MPU_LDS_TABLES
-#define PSGPU_MPU_LDS_TABLES 1  // k_mpu gathers its MC table words from an LDS copy (A/B knob)
-#endif
-constexpr int kLdsTabOff = kMpusPerBlock * kLdsMpu;  // the block's copy of the tables
-constexpr int kLdsWaveSlots = kLdsTabOff + (PSGPU_MPU_LDS_TABLES ? kLdsTables : 0);  // interpreter slots follow
+constexpr int kLdsWaveSlots = kMpusPerBlock * kLdsMpu;  // interpreter slots follow
 
 // Last cell c in [0, 343) with first[c] <= r (first[] = exclusive prefix of per-cell
 // counts, non-decreasing, first[0] = 0, so that cell holds item r): binary lifting,
@@ -1169,21 +1162,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     phase_stamp(p, 0);
     const uint32_t d = blockIdx.x * (uint32_t)MPB + (uint32_t)slot;
     ModelPtr M = as_const(p.model);
-#if PSGPU_MPU_LDS_TABLES
-    // the MC tables passes 1-3 gather from (5.9 KB) copied into the block's LDS while wave 0
-    // reads the shard counts, one barrier for both: each gather then costs an LDS round trip
-    // (~50 cycles) instead of an L1 / L2 one (~200; MI355X_MICROARCH.md).  Not in the tree-split
-    // kernel, whose own LDS already limits it to 5 blocks per CU (it is launched without room)
-    const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
-    if constexpr (SPLIT == 1) {
-        const uint4* src = reinterpret_cast<const uint4*>(p.tables);
-        uint4* dst = reinterpret_cast<uint4*>(smem + kLdsTabOff);
-        for (int i = (int)threadIdx.x; i < kLdsTables / 16; i += (int)blockDim.x) dst[i] = src[i];
-        tab = reinterpret_cast<const CubeTablesDev*>(smem + kLdsTabOff);
-    }
-#else
-    const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident
-#endif
+    const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident (an LDS copy per block measured slower, r05)
     // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
     // the block
     __shared__ uint32_t sIncl[kShards];
@@ -1337,29 +1316,19 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         const bool cellLane = j < 7 && k < 7;
         const uint32_t ownJK = tab->own[(j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];    // cells with i > 0
         const uint32_t ownJK0 = tab->own[4 | (j == 0 ? 2 : 0) | (k == 0 ? 1 : 0)];  // the i == 0 slab
-        // the 7 slabs' configurations first and their table words loaded together (one
-        // latency instead of 7 in a row: each slab's scan needs its word; crossNtri[0] and
-        // crossNtri[255] are 0, so the load needs no condition)
-        uint32_t cfgs[7], cns[7];
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-            const uint32_t b0 = (uint32_t)(ins[i] >> lane), b1 = (uint32_t)(ins[i + 1] >> lane);
-            cfgs[i] = cellLane ? ((b0 & 3u) | ((b0 >> 6) & 12u) | ((b1 & 3u) << 4) | (((b1 >> 8) & 3u) << 6)) : 0u;
-        }
-#if PSGPU_PASS1_HOIST
-#pragma unroll
-        for (int i = 0; i < 7; ++i) cns[i] = tab->crossNtri[cfgs[i]];
-#endif
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
             const int c = i * 49 + j * 7 + k;
-            const uint32_t cfg = cfgs[i];
-#if PSGPU_PASS1_HOIST
-            const uint32_t cn = cns[i];
-#else
-            const uint32_t cn = (cfg != 0 && cfg != 255) ? tab->crossNtri[cfg] : 0u;  // r04: loaded per slab
-#endif
-            const uint32_t nvt = (uint32_t)__popc((i == 0 ? ownJK0 : ownJK) & cn & 0xfffu) | (cn & 0xffff0000u);
+            const uint32_t b0 = (uint32_t)(ins[i] >> lane), b1 = (uint32_t)(ins[i + 1] >> lane);
+            uint32_t cfg = 0;
+            if (cellLane)
+                cfg = (b0 & 3u) | ((b0 >> 6) & 12u) | ((b1 & 3u) << 4) | (((b1 >> 8) & 3u) << 6);
+            uint32_t nvt = 0;
+            if (cfg != 0 && cfg != 255)
+            {
+                const uint32_t cn = tab->crossNtri[cfg];
+                nvt = (uint32_t)__popc((i == 0 ? ownJK0 : ownJK) & cn & 0xfffu) | (cn & 0xffff0000u);
+            }
             const uint32_t svt = wave_incl_scan(nvt);  // one scan for both counts
             if (cellLane && part == 0) {
                 const uint32_t first = carry + svt - nvt;

@@ -579,7 +579,7 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, split ? mpu_split_lds_bytes() : mpu_lds_bytes(0), s, p));
+    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)

@@ -146,7 +146,6 @@ __global__ void __launch_bounds__(256) k_export_pack(PackSrc src, uint32_t* __re
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (psgpu_launch.h).
 size_t mpu_lds_bytes(uint32_t slots) { return kLdsWaveSlots + 4 * ((size_t)slots * 64 * 4); }
-size_t mpu_split_lds_bytes() { return kLdsTabOff; }  // the tree-split k_mpu keeps its tables global
 size_t walk_lds_bytes(uint32_t slots) { return 4 * ((size_t)slots * 4 * 64 * 4); }
 size_t precheck_lds_bytes(uint32_t slots) { return 4 * ((size_t)slots * 64 * 4); }
 

@@ -9,7 +9,6 @@
 namespace psgpu {
 
 size_t mpu_lds_bytes(uint32_t slots);
-size_t mpu_split_lds_bytes();
 size_t walk_lds_bytes(uint32_t slots);
 size_t precheck_lds_bytes(uint32_t slots);
 hipError_t launch_precheck(const Params& p, hipStream_t s);

@@ -147,6 +147,23 @@ def test_jit_compiles_c3(mode):
     assert gpu.jit_compile(m, mode) > 10000
 
 
+def test_generated_kernels_resources():
+    """Registers, LDS and scratch of C3's generated kernels (tools/kernel_resources.py, the
+    code object's metadata; DESIGN.md §4 "Round 5: occupancy"): no spills, no scratch, and
+    the occupancy each hot kernel was measured at -- a change that costs a wave per SIMD
+    shows up here before it reaches a GPU."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as kr
+
+    ks = kr.compile_variant("C3", 1 | 4, {})
+    floor = {"jit_precheck": 7, "jit_mpu": 6, "jit_vertex": 8, "jit_vertex_w": 8, "jit_finish": 7,
+             "jit_finish_p": 7, "jit_finish_q": 6, "jit_precheck_s": 7, "jit_mpu_s": 5}
+    for name, want in floor.items():
+        r = ks[name]
+        assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["sgpr_spill"] == 0, (name, r)
+        assert r["waves_per_simd"] >= want, (name, r["waves_per_simd"], r["limited_by"], r["vgpr"], r["sgpr"])
+
+
 _JIT_TREES = r"""
 import os, sys
 sys.path.insert(0, os.environ["PSGPU_ROOT"])
