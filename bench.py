@@ -461,7 +461,6 @@ def main():
                          "launches that queue few MPUs (default: 2 for strong scaling over N > 1 ranks, whose "
                          "shares are small, else 0)")
     ap.add_argument("--debug", type=int, default=0, help=argparse.SUPPRESS)  # profiling ablations only
-    ap.add_argument("--stagger-us", type=float, default=0.0, help=argparse.SUPPRESS)  # experiments only
     ap.add_argument("--vertex-blocks", type=int, default=0, help=argparse.SUPPRESS)  # persistent grids (experiments)
     ap.add_argument("--finish-blocks", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -639,10 +638,6 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):  # step k is one complete polygonization, on engine k mod E
         engines[k % neng].polygonize()
-        if k < neng - 1 and args.stagger_us > 0:  # experiment: the first round's engines start apart
-            ts = time.perf_counter() + args.stagger_us * 1e-6
-            while time.perf_counter() < ts:
-                pass
     t_enq = time.perf_counter()
     results = [e.finish() for e in engines]
     grp.barrier()

@@ -73,9 +73,14 @@ def main():
                 st = (s[r, :, 0] - lo) * TICK_US
                 en = (s[r, :, 1] - lo) * TICK_US
                 ends.append(en[-1])
-                if rep == a.reps - 1:
+                if rep == a.reps - 1 and a.steps <= 40:
                     print(f"  engine {ei} step {r * E + ei:2d}: " +
                           " | ".join(f"{k[2:]} {st[i]:7.1f}-{en[i]:7.1f}" for i, k in enumerate(gpu.STAMP_KERNELS)))
+        # round k = steps [kE, (k+1)E): from engine 0's step start to the next round's
+        starts0 = (sp[0][:, 0, 0] - lo) * TICK_US
+        rounds = np.diff(starts0)
+        print(f"  rounds (engine 0 step to step, us): {' '.join(f'{x:.0f}' for x in rounds[:12])}"
+              f"{' ...' if len(rounds) > 12 else ''} {' '.join(f'{x:.0f}' for x in rounds[-6:]) if len(rounds) > 12 else ''}")
         ends = np.sort(np.array(ends))
         gaps = np.diff(ends)
         print(f"  step completions (us): first {ends[0]:.1f}, then every {np.median(gaps):.1f} (median), last {ends[-1]:.1f}")
