@@ -733,6 +733,9 @@ __device__ __forceinline__ void phase_stamp(const Params& p, int ph, uint32_t bi
 // The same, taken only once `dep` has been computed (inline asm keeps the clock read after its
 // producer and in program order with the other stamps): phases of k_finish (debug bit 2048;
 // the stamps change the kernel's registers, so they exist only when PSGPU_FIN_PHASES is 1).
+#ifndef PSGPU_MPU_LIVE_STAMP
+#define PSGPU_MPU_LIVE_STAMP 0  // k_mpu's live-primitive word: measurement builds only (PSGPU_JIT_FLAGS)
+#endif
 #ifndef PSGPU_FIN_PHASES
 #define PSGPU_FIN_PHASES 0  // compiled in only for the measurement (PSGPU_JIT_FLAGS=-DPSGPU_FIN_PHASES=1)
 #endif
@@ -1352,6 +1355,15 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         }
     }
     phase_stamp(p, 5);
+#if PSGPU_MPU_LIVE_STAMP
+    // phase word 7 (measurement builds only): the wave's live primitives, its MPU's V and T
+    if ((p.debug & 4096u) && p.stamps && lane == 0 && live) {
+        const uint32_t sw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (sw < p.stampCap)
+            p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)sw + 7] =
+                (uint64_t)(128 - __popcll(cm.lo) - __popcll(cm.hi)) | ((uint64_t)V << 16) | ((uint64_t)T << 32);
+    }
+#endif
     mpu_sync<WPM>();
     const bool recs = work && !(p.debug & 2u);  // ablation bit 1: pass 1 only
     const uint32_t shard = d & (kShards - 1);
@@ -2026,6 +2038,15 @@ if constexpr (VPW == 16) {
                 else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
             }
             phase_stamp_after(p, 3, 2048u, __uint_as_float((uint32_t)(cm.lo ^ cm.hi)));
+#if PSGPU_FIN_PHASES
+            const uint64_t nvalid = (uint64_t)__popcll(ballot(valid));
+            if ((p.debug & 2048u) && p.stamps && lane == 0) {  // phase word 7: live primitives, vertices
+                const uint32_t sw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+                if (sw < p.stampCap)
+                    p.stamps[3 * (size_t)kNumStampKernels * p.stampCap + 8 * (size_t)sw + 7] =
+                        (uint64_t)(128 - __popcll(cm.lo) - __popcll(cm.hi)) | (nvalid << 16);
+            }
+#endif
             // value + colour at p and the normal's per-point fieldValue at p + delta*e_a
             // (:1598-1622) as four points of one walk (the colour of points 1-3 is dead
             // code); then SimdNormalize (rsqrt -> IEEE 1/sqrtf)

@@ -130,6 +130,31 @@ def mpu_phases(config="C3", share=1):
             print(f"  {nm:15s} median {np.median(dt):6.2f} us  p90 {np.percentile(dt, 90):6.2f}  max {dt.max():6.2f}")
     st = (ph[real, 0] - t0) * TICK_US
     print(f"  wave entry time: median {np.median(st):.2f} us, p90 {np.percentile(st, 90):.2f}, max {st.max():.2f}")
+    w7 = ph[:, 7]
+    if (w7[real] != 0).any():  # built with -DPSGPU_MPU_LIVE_STAMP=1: live primitives, V, T per wave
+        live = (w7 & 0xFFFF) - (128 - model.ct_prims)
+        V = (w7 >> 16) & 0xFFFF
+        T = (w7 >> 32) & 0xFFFF
+        s2 = (ph[:, 3] - ph[:, 2]) * TICK_US
+        life = (rec[:, 1] - rec[:, 0]) * TICK_US
+        _live_table("k_mpu", live, real, {"S2 walk": s2, "life": life}, {"V": V, "T": T})
+
+
+def _live_table(kernel, live, real, times, counts):
+    """Per bucket of live primitives: waves, the summed counts (vertices / triangles), the
+    p50 / max of each phase -- how much of the work sits in the heavy waves that set the span."""
+    print(f"  {kernel} by live primitives:")
+    tot = {k: max(1, int(v[real].sum())) for k, v in counts.items()}
+    for lo, hi in ((0, 4), (4, 8), (8, 12), (12, 16), (16, 20), (20, 24), (24, 28), (28, 33)):
+        sel = real & (live >= lo) & (live < hi)
+        if not sel.any():
+            continue
+        line = f"    [{lo:2d},{hi:2d}): waves {int(sel.sum()):5d}"
+        for k, v in counts.items():
+            line += f"  {k} {int(v[sel].sum()):7d} ({100 * v[sel].sum() / tot[k]:4.1f} %)"
+        for k, v in times.items():
+            line += f"  {k} p50 {np.median(v[sel]):5.2f} max {v[sel].max():5.2f}"
+        print(line)
 
 
 def precheck_phases(config="C3", share=1):
@@ -214,6 +239,13 @@ def finish_phases(config="C3", share=1):
     st = (rec[real, 0] - t0) * TICK_US
     print(f"  life median {np.median(life):.2f} p90 {np.percentile(life, 90):.2f} max {life.max():.2f}; "
           f"start median {np.median(st):.2f} max {st.max():.2f}")
+    w7 = ph[:, 7]
+    if (w7[real] != 0).any():  # live primitives and vertices per wave (PSGPU_FIN_PHASES builds)
+        live = (w7 & 0xFFFF) - (128 - model.ct_prims)
+        nv = (w7 >> 16) & 0xFFFF
+        walk = (ph[:, 4] - ph[:, 3]) * TICK_US
+        lifeall = (rec[:, 1] - rec[:, 0]) * TICK_US
+        _live_table("k_finish", live, real, {"walk": walk, "life": lifeall}, {"vertices": nv})
     # the waves that end last: what they spent their time on
     worst = np.argsort(rec[:, 1])[-8:]
     for w in worst:
