@@ -579,7 +579,8 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0), s, p));
+    // the split kernel's blocks hold 2 MPUs, the others 4 (mpu_lds_bytes(0): 4 MPUs' LDS)
+    if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0) / (split ? 2 : 1), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)

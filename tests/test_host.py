@@ -157,7 +157,7 @@ def test_generated_kernels_resources():
 
     ks = kr.compile_variant("C3", 1 | 4, {})
     floor = {"jit_precheck": 7, "jit_mpu": 6, "jit_vertex": 8, "jit_vertex_w": 8, "jit_finish": 7,
-             "jit_finish_p": 7, "jit_finish_q": 6, "jit_precheck_s": 7, "jit_mpu_s": 5}
+             "jit_finish_p": 7, "jit_finish_q": 6, "jit_precheck_s": 7, "jit_mpu_s": 7}
     for name, want in floor.items():
         r = ks[name]
         assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["sgpr_spill"] == 0, (name, r)

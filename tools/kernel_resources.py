@@ -6,7 +6,8 @@ Occupancy rules (MI355X_MICROARCH.md "Register files", "Residency"): 256-thread 
 wave per SIMD each); waves/SIMD by VGPRs = min(8, 512 // alloc), alloc = VGPR + AGPR rounded
 up to 8; blocks/CU by SGPRs = min(8, 800 // (ceil(sgpr / 16) * 16 + 16)); blocks/CU by LDS =
 163840 // (static + dynamic LDS); at most 8 blocks (32 waves) per CU.  k_mpu's dynamic LDS is
-the host's mpu_lds_bytes(0) = 4 MPUs x 4,864 B (psgpu_device.h kLdsMpu); the others take none.
+the host's mpu_lds_bytes(0) = 4 MPUs x 4,864 B (psgpu_device.h kLdsMpu), half that for the
+tree-split k_mpu (2 MPUs per block); the others take none.
 
 Static instruction mix per kernel from llvm-objdump (VALU = v_* except v_readlane /
 v_readfirstlane / v_writelane counted as VALU too; s_nop; s_waitcnt; packed fp32).
@@ -26,8 +27,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-K_LDS_MPU = 4864            # psgpu_device.h kLdsMpu
+K_LDS_MPU = 4864            # psgpu_device.h kLdsMpu (6400 with PSGPU_MPU_MAPS 1)
 MPU_DYNAMIC_LDS = 4 * K_LDS_MPU  # mpu_lds_bytes(0), kMpusPerBlock = 4 (PSGPU_MPU_WAVES 1)
+MPU_S_DYNAMIC_LDS = 2 * K_LDS_MPU  # the tree-split k_mpu: 2 MPUs per block
 ROLE = {"jit_precheck": "k_precheck", "jit_mpu": "k_mpu", "jit_vertex": "k_vertex (quad, 16/wave)",
         "jit_vertex_w": "k_vertex (wide, 64/wave)", "jit_finish": "k_finish (64/wave)",
         "jit_finish_q": "k_finish (quad, 16/wave)", "jit_finish_p": "k_finish (pair, 32/wave)",
@@ -121,7 +123,7 @@ def compile_variant(config: str, mode: int, env: dict) -> dict:
     out = {}
     for name, r in sorted(meta.items()):
         out[name] = {"role": ROLE.get(name, name), **r,
-                     **occupancy(r, MPU_DYNAMIC_LDS if name in ("jit_mpu", "jit_mpu_s") else 0),
+                     **occupancy(r, MPU_DYNAMIC_LDS if name == "jit_mpu" else MPU_S_DYNAMIC_LDS if name == "jit_mpu_s" else 0),
                      **mix.get(name, {})}
     return out
 
