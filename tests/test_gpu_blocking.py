@@ -175,3 +175,30 @@ def test_cpp_ps_simdpoly_polygonize_mpustats(tmp_path):
     assert (ps["idxThread"] == -7).all() and (ps["bIntersected"] == np.arange(ct)).all()
     assert (ps["tickEnd"] >= ps["tickStart"]).all()
     assert (ps["tickStart"] >= t0 - 50_000).all() and (ps["tickEnd"] <= t1 + 50_000).all()
+
+
+def test_blocking_export_fuzz_sequence(oracle):
+    """The blocking export over the fuzz trees (tests/test_gpu_fuzz.py: every node type, cell
+    sizes off the round values) on one context, one after the other -- the mesh and the
+    lattice shrink and grow under the same staging -- with both test hooks on: every PolyMPUs
+    equals the live oracle's output for its tree."""
+    import test_gpu_fuzz as fz
+
+    p = gpu.Polygonizer(0)
+    try:
+        p.set_option(gpu.OPT_DEBUG, gpu.DEBUG_EXPORT_POISON | gpu.DEBUG_EXPORT_STRAGGLER)
+        for seed in range(0, 40, 3):
+            model, cs = fz.fuzz_case(seed)[:2]
+            n = gpu.count_mpus(cs, *model.bbox)
+            mpus = np.zeros(n, soa.MPU_DTYPE)
+            stats = np.zeros(n, soa.MPU_STATS_DTYPE)
+            rc, ct, _ = p.polygonize_mpus(cs, model, mpus, stats)
+            om = oracle.polygonize(model, cs, 0, 0xFFFFFFFF, threads=8)
+            if rc == soa.RET_MPU_VT_OVERFLOW:  # an MPU past the reference's 512 V / T
+                assert (om.stats[:, 2:4] > 512).any(), seed
+                continue
+            assert rc == soa.RET_SUCCESS and ct == n, (seed, rc, ct)
+            want = mesh_digests(om.stats[:, :4], om.pos, om.nrm, om.col, om.tris)
+            assert polympus_digests(mpus, stats) == want, seed
+    finally:
+        p.close()
