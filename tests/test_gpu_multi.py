@@ -362,3 +362,37 @@ def test_bench_two_ranks_strong_split_one_device():
     per = out["mesh"]["per_rank"]
     assert sum(p[1] for p in per) == 339820 and sum(p[2] for p in per) == 520224
     assert sum(p[0] for p in per) == 50653
+
+
+@pytest.mark.parametrize("seed", [0, 4, 9, 13, 19, 38])
+def test_group_fuzz_random_splits(group8, oracle, seed):
+    """The fuzz trees (tests/test_gpu_fuzz.py) over 8 parts of one device at random split
+    points (empty parts included): the reassembled mesh is the oracle's, and the device gather
+    (peer copies + rebase kernel) equals it."""
+    import ctypes
+
+    import test_gpu_fuzz as fz
+
+    model, cs = fz.fuzz_case(seed)[:2]
+    n = gpu.count_mpus(cs, *model.bbox)
+    rng = np.random.default_rng(seed)
+    inner = sorted(int(x) for x in rng.integers(0, n + 1, 7))
+    group8.set_model(model)
+    group8.set_split([0] + inner + [n])
+    info, parts = group8.run(cs)
+    assert [p.mpuBegin for p in parts] == [0] + inner and info.ctMPUs == n
+    mesh = group8.download()
+    om = oracle.polygonize(model, cs, threads=8)
+    assert_mesh_matches(mesh, np.concatenate(_group_stats(group8)), om)
+    V, T = info.ctVertices, info.ctTriangles
+    if V == 0:
+        return
+    d = group8.gather(0)
+    pos = np.zeros((V, 3), np.float32)
+    tris = np.zeros((T, 3), np.uint32)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(pos.ctypes.data, d.pos, pos.nbytes, 2) == 0
+    assert hip.hipMemcpy(tris.ctypes.data, d.tris, tris.nbytes, 2) == 0
+    assert_bits_equal(pos, mesh.pos, "gathered positions")
+    np.testing.assert_array_equal(tris, mesh.tris)
