@@ -28,11 +28,14 @@ def run(a):
     model, cs, N = synth.make_config(a.config)
     E = a.engines
     eng = [gpu.Polygonizer(0) for _ in range(E)]
-    for e in eng:
+    for i, e in enumerate(eng):
         e.set_option(gpu.OPT_JIT, gpu.JIT_STRUCTURE)
         if E > 1:  # bench.py's grids with several engines
             e.set_option(gpu.OPT_VERTEX_BLOCKS_PER_CU, 8)
             e.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, 4)
+        if a.mix and i % 2 == 1:  # every second engine on other layouts: chains of other lengths
+            e.set_option(gpu.OPT_FINISH_QUAD, a.mix_fquad)
+            e.set_option(gpu.OPT_VERTEX_WIDE, a.mix_vwide)
         e.set_model(model)
     for rep in range(a.reps):
         for K, W in [(int(x), int(w)) for x in a.ks.split(",") for w in a.warmups.split(",")]:
@@ -128,6 +131,9 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--parse", default=None, help="a rocprofv3 kernel_trace.csv (or a directory holding one)")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--mix", action="store_true", help="odd engines take --mix-fquad / --mix-vwide layouts")
+    ap.add_argument("--mix-fquad", type=int, default=3)
+    ap.add_argument("--mix-vwide", type=int, default=0)
     a = ap.parse_args()
     if a.parse:
         parse(a)
