@@ -868,7 +868,10 @@ def main():
                    "parallelism": f"{scaling}-{grp.world}gpu", "engines_per_gpu": neng, "parts_per_engine": nparts,
                    "streams_per_gpu": neng * nparts,
                    "persistent_blocks_per_cu": [args.vertex_blocks or (8 if neng > 1 else 16),
-                                                args.finish_blocks or (4 if neng > 1 else 8)], "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                                                args.finish_blocks or (4 if neng > 1 else 8)],
+                   "grids": "k_vertex / k_finish: a wave per batch of the last run's vertices + 1/8, at most "
+                            "the persistent grids" if os.environ.get("PSGPU_GRID_FIT", "1") != "0" else "persistent",
+                   "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                    "step": "one complete polygonization of the rank's MPU range (all four kernels); steps "
                            "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,

@@ -988,7 +988,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (jitEnv) c->useJit = std::min(3, std::max(0, atoi(jitEnv)));
     const char* asyncEnv = getenv("PSGPU_JIT_ASYNC");
     if (asyncEnv) c->jitAsync = atoi(asyncEnv) != 0;
-    if (const char* e = getenv("PSGPU_GRID_FIT")) c->gridFit = atoi(e) != 0;          // A/B tooling
+    if (const char* e = getenv("PSGPU_GRID_FIT")) c->gridFit = atoi(e) != 0;          // 0: persistent grids
     if (const char* e = getenv("PSGPU_FINISH_QUAD")) c->finishQuad = std::min(3, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_VERTEX_WIDE")) c->vertexWide = std::min(2, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_MPU_MARGIN")) c->mpuMarginDiv = std::max(1, atoi(e));

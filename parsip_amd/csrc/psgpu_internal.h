@@ -72,7 +72,9 @@ struct psgpu_ctx {
     uint32_t splitMaxQueued = 1024;  // PSGPU_OPT_SPLIT_MAX_QUEUED: tree split 2 applies up to this many S2 MPUs
                                      // (psgpu_create: 4 per CU; C3's 1/8 shares queue ~800, 1/4 ~1,600)
     uint32_t runMpb = 0;      // k_mpu MPUs per block of the last enqueued run
-    int gridFit = 0;          // k_vertex / k_finish grids sized from the last run's vertices
+    int gridFit = 1;          // k_vertex / k_finish grids sized from the last run's vertices, capped
+                              // at the persistent grids (PSGPU_GRID_FIT=0: the persistent grids;
+                              // C4 1/8 shares -5 %, full grids neutral: profiles/r05_grid_fit_ab2.txt)
     int mpuMarginDiv = 4;     // k_mpu grid: last run's queued MPUs + 1/this (re-run if short)
     int vertexWide = 2;  // PSGPU_OPT_VERTEX_WIDE: 0 a quad, 1 one lane per vertex, 2 by the last run's vertex count
     uint32_t lastV = 0;  // vertices of the last finished run (0: none yet)
