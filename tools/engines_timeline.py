@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--steps", type=int, default=40, help="queued steps before the recorded ones")
     ap.add_argument("--json")
+    ap.add_argument("--share", type=int, default=1, help="time rank --rank's range of a cost split in SHARE parts")
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--tree-split", type=int, default=0, help="PSGPU_OPT_TREE_SPLIT (bench.py: 2 for N > 1 ranks)")
     a = ap.parse_args()
     model, cs, N = synth.make_config(a.config)
     # Three sets of E contexts with stamps on (a context's stamps hold its last run): set A takes
@@ -62,16 +65,24 @@ def main():
     stream_of = {id(c): streams[i % E] for st in sets for i, c in enumerate(st)}
     for e in allc:
         e.set_option(gpu.OPT_JIT, gpu.JIT_STRUCTURE)
+        e.set_option(gpu.OPT_TREE_SPLIT, a.tree_split)
+        if E > 1:  # bench.py's grids with several engines
+            e.set_option(gpu.OPT_VERTEX_BLOCKS_PER_CU, 8)
+            e.set_option(gpu.OPT_FINISH_BLOCKS_PER_CU, 4)
         e.set_model(model)
         e.set_option(gpu.OPT_STAMPS, 1 << 15)
+    lo, hi = 0, None
+    if a.share > 1:
+        b = allc[0].plan_split(cs, a.share)
+        lo, hi = int(b[a.rank]), int(b[a.rank + 1])
     for k in range(a.warmup):
         c = allc[k % len(allc)]
-        c.polygonize(cs, stream=stream_of[id(c)])
+        c.polygonize(cs, lo, hi, stream=stream_of[id(c)])
     for e in allc:
         e.finish()
     seq = [sets[0][k % E] for k in range(a.steps)] + (sets[1] + sets[2] if E > 1 else [])
     for e in seq:
-        e.polygonize(cs, stream=stream_of[id(e)])
+        e.polygonize(cs, lo, hi, stream=stream_of[id(e)])
     for e in allc:
         e.finish()
     runs = [e.stamps() for st in sets for e in st]
@@ -79,7 +90,7 @@ def main():
     focus = [i for i, e in enumerate(c for st in sets for c in st) if e in tset]
     t_first = min(int(runs[i][k][:, 0].min()) for i in focus for k in gpu.STAMP_KERNELS if len(runs[i][k]))
     t_last = max(int(runs[i][k][:, 1].max()) for i in focus for k in gpu.STAMP_KERNELS if len(runs[i][k]))
-    out = {"engines": a.engines, "config": a.config, "env": {k: v for k, v in os.environ.items() if k.startswith("PSGPU")},
+    out = {"engines": a.engines, "config": a.config, "share": [a.share, a.rank, lo, hi], "env": {k: v for k, v in os.environ.items() if k.startswith("PSGPU")},
            "window_us": round((t_last - t_first) * TICK_US, 2), "kernels": {}}
     # all waves: (kernel index, engine, start, end, simd)
     rows = []
