@@ -67,7 +67,13 @@ def main():
         ps = [subprocess.Popen([sys.executable, __file__, "--procs", str(a.procs), "--engines", str(a.engines),
                                 "--steps", str(a.steps), "--rank", str(r), "--dir", d], stdout=subprocess.PIPE, text=True)
               for r in range(a.procs)]
-        outs = [p.communicate(timeout=300)[0] for p in ps]
+        try:
+            outs = [p.communicate(timeout=300)[0] for p in ps]
+        except subprocess.TimeoutExpired:
+            for p in ps:  # never leave a child behind on the GPU
+                p.kill()
+                p.wait()
+            sys.exit("a child did not finish within 300 s")
     if any(p.returncode for p in ps):
         sys.exit(f"a child failed: {[p.returncode for p in ps]}")
     res = [json.loads(o.strip().splitlines()[-1]) for o in outs]
