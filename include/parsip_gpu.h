@@ -284,8 +284,11 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        staging past the piece flags is filled with the call's
                                        epoch before the export / the packing kernel's last
                                        block waits ~40 us before each piece */
-#define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU */
-#define PSGPU_OPT_FINISH_BLOCKS_PER_CU 5  /* persistent k_finish grid */
+#define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU; once a
+                                             run of the same range has finished, the grid is fitted
+                                             to its vertices (+1/8) up to this (env PSGPU_GRID_FIT=0:
+                                             always the persistent grid) */
+#define PSGPU_OPT_FINISH_BLOCKS_PER_CU 5  /* persistent k_finish grid (fitted the same way) */
 #define PSGPU_OPT_GRAPH         7   /* 1: replay repeated launch sequences from a hipGraph (off by
                                        default: +4-5 us per polygonization on ROCm 7.2) */
 #define PSGPU_OPT_CAPACITY      6   /* restart output buffers at this vertex capacity (>= 64;
