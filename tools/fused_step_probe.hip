@@ -62,12 +62,12 @@ __device__ __forceinline__ bool grid_barrier(const Bar& b, unsigned int phase) {
     return sOk != 0;
 }
 
-// launch n of an engine: its barriers are phases 3n, 3n + 1, 3n + 2 of monotonic counters
-// (no reset between launches, so no memset joins the step)
-__global__ void __launch_bounds__(256) k_fused(Arg a, Bar b, unsigned int n) {
+// launch n of an engine: its barriers are phases nbar n .. nbar n + nbar - 1 of monotonic
+// counters (no reset between launches, so no memset joins the step)
+__global__ void __launch_bounds__(256) k_fused(Arg a, Bar b, unsigned int n, unsigned int nbar) {
     if (a.w[0] == 0xdeadbeefu && threadIdx.x == 1234567) a.w[1] = 0;
-    for (unsigned int ph = 0; ph < 3; ++ph)
-        if (!grid_barrier(b, 3u * n + ph)) return;  // every block leaves: the error word says why
+    for (unsigned int ph = 0; ph < nbar; ++ph)
+        if (!grid_barrier(b, nbar * n + ph)) return;  // every block leaves: the error word says why
 }
 
 #define CHECK(x)                                                     \
@@ -110,7 +110,20 @@ int main(int argc, char** argv) {
                    (t1 - t0) / steps);
             fflush(stdout);
         }
-        for (int perCu : {1, 2}) {
+        {  // two kernels per step (k_precheck + k_mpu and k_vertex + k_finish each fused)
+            const double t0 = now_us();
+            for (int s = 0; s < steps; ++s) {
+                hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, st[s % E], a);
+                hipLaunchKernelGGL(k_empty, dim3(chain[2]), dim3(256), 0, st[s % E], a);
+            }
+            CHECK(hipDeviceSynchronize());
+            const double t1 = now_us();
+            printf("engines %d chain2 (256 | %u blocks): %.2f us/step\n", E, chain[2], (t1 - t0) / steps);
+            fflush(stdout);
+        }
+        for (int cfg = 0; cfg < 4; ++cfg) {
+            const int perCu = cfg == 3 ? 2 : 1;
+            const unsigned int nbar = cfg == 0 ? 0u : (cfg == 1 ? 1u : 3u);
             const unsigned int B = (unsigned)(perCu * cus);
             for (auto& m : mem) CHECK(hipMemset(m, 0, words * 4));
             unsigned int err = 0;
@@ -118,7 +131,7 @@ int main(int argc, char** argv) {
             for (int s = 0; s < steps; ++s) {
                 const int e = s % E;
                 Bar b{mem[e], mem[e] + 8 * 32, mem[e] + 8 * 32 + 32, B / 8u, 8u, 1u << 22};
-                hipLaunchKernelGGL(k_fused, dim3(B), dim3(256), 0, st[e], a, b, (unsigned)(s / E));
+                hipLaunchKernelGGL(k_fused, dim3(B), dim3(256), 0, st[e], a, b, (unsigned)(s / E), nbar);
             }
             CHECK(hipDeviceSynchronize());
             const double t1 = now_us();
@@ -127,7 +140,7 @@ int main(int argc, char** argv) {
                 CHECK(hipMemcpy(&x, mem[e] + 8 * 32 + 32, 4, hipMemcpyDeviceToHost));
                 err |= x;
             }
-            printf("engines %d fused  (%u blocks, 3 grid barriers): %.2f us/step%s\n", E, B, (t1 - t0) / steps,
+            printf("engines %d fused  (%u blocks, %u grid barriers): %.2f us/step%s\n", E, B, nbar, (t1 - t0) / steps,
                    err ? "  [a barrier spin gave up]" : "");
             fflush(stdout);
         }
