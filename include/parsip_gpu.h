@@ -333,6 +333,11 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        whole tree.  Non-zero compiles the split kernels too (+30-45 %
                                        hiprtc time).  Identical output */
 #define PSGPU_OPT_SPLIT_MAX_QUEUED 17  /* threshold of PSGPU_OPT_TREE_SPLIT 2 (default 4 per CU) */
+#define PSGPU_OPT_FUSED_SURFACE 21  /* k_vertex + k_finish as one launch (quad layouts, the offsets
+                                       scan released inside it): 2 (default) for runs whose last
+                                       run's vertices take the quad layouts in both (small rank
+                                       shares), 1 always, 0 never.  Needs the small-launch kernels,
+                                       compiled with PSGPU_OPT_TREE_SPLIT != 0.  Identical output */
 #define PSGPU_OPT_MPU_TICKS    19   /* 1: runs record per-MPU ticks for MPUSTATS
                                        (psgpu_download_process_stats); 0 (default) off */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the

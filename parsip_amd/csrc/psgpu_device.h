@@ -2106,6 +2106,170 @@ if constexpr (VPW == 16) {
     phase_stamp_after(p, 6, 2048u, 0.0f);
 }
 
+// k_surface's wait for the offsets scan (every scan block released its offsets), bounded: a
+// broken protocol flags the run (error bit 1) instead of hanging the device.
+__device__ __forceinline__ void surface_wait_scan(const Params& p) {
+    if (lane_id() == 0) {
+        uint32_t spins = 0;
+        while (__hip_atomic_load(&p.ctr->scanDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.scanBlocks) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) {  // block 0 published the counters long before: flag
+                atomicOr(&p.ctr->error, 2u);  // the run's totals and the host copy as well
+                atomicOr(&p.totals[7], 2u);
+                p.hostCtr->error = p.hostCtr->error | 2u;
+                __threadfence_system();
+                break;
+            }
+        }
+    }
+    // no agent-scope acquire here: on gfx950 it invalidates the XCD's L2 for every kernel on it
+    // (measured: a 1/8 share 0.028 vs 0.015 ms/step).  The offsets are read with agent-scope
+    // loads instead (surface_offs), which bypass the non-coherent caches and are issued only
+    // after the flag was seen.
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+// an offsets word written by this launch's scan blocks (released before their scanDone count)
+__device__ __forceinline__ uint64_t surface_offs(const Params& p, uint32_t i) {
+    return __hip_atomic_load(&p.offs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// k_surface (PSGPU_OPT_FUSED_SURFACE): k_vertex and k_finish in one launch for small launches
+// (a rank's share; the launch floor, not the work, sets their step: DESIGN.md §5).  A quad of
+// lanes per vertex for both walks -- the root's 4 edge samples (k_vertex's quad layout), then
+// value + colour at the root and its 3 normal samples (k_finish's quad layout) -- with the
+// root's bracket and scale kept in registers instead of the vertex record.  The first blocks
+// run the offsets scan as in k_vertex and release it; a wave waits for every scan block only
+// before its first mesh write.  Same values as the two kernels: the same expressions on the
+// same records and the same culling masks.  The scan blocks have the lowest block ids, so they
+// are dispatched before any waiting block of their XCD: the wait cannot starve them.
+template <class EV>
+__device__ __forceinline__ void surface_body(const Params& p, float* lds) {
+    const int wave = wave_index();
+    const int lane = lane_id();
+    ModelPtr M = as_const(p.model);
+    EV ev(M, lds + wave * (p.slotsPerLane * 4 * 64) + lane);
+    const uint32_t nWaves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + wave;
+    const float delta = 0.001f;
+    const float inv = -1.0f / delta;
+    if (blockIdx.x < p.scanBlocks) {  // block-uniform
+        scan_counts_block(p, blockIdx.x);
+        __syncthreads();  // the block's offsets stores are in L2
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // ... and written back for the other XCDs
+            __hip_atomic_fetch_add(&p.ctr->scanDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (blockIdx.x == 0) {  // k_finish's block-0 duties (finish_body)
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.ctr);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(p.hostCtr);
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) dst[i] = src[i];
+        __threadfence_system();
+        uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
+        for (uint32_t i = threadIdx.x; i < kScanMaxBlocks; i += blockDim.x) p.scanStatusNext[i] = 0ull;
+        if (threadIdx.x < 64) {
+            const ShardCtr& sc = p.ctr->shard[threadIdx.x];
+            const uint32_t tv = wave_sum(sc.v), tt = wave_sum(sc.t), tp = wave_sum(sc.p), tb = wave_sum(sc.b),
+                           ts = wave_sum(sc.s);
+            if (threadIdx.x == 0) {
+                const uint32_t tot[8] = {p.mpuCount, tv, tt, tp + tb, ts, tp, (uint32_t)p.ctr->firstOverflow,
+                                         p.ctr->error};
+                for (int i = 0; i < 8; ++i) p.totals[i] = tot[i];
+            }
+        }
+    }
+    __shared__ uint32_t sCnt[2 * kShards];
+    stage_shard_counts(p, 1, sCnt);            // ShardCtr::v
+    stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
+    __syncthreads();
+    bool scanSeen = false;
+    const ShardBatches sv(sCnt, p.vShardCap, 16);
+    const int qj = lane & 3;
+    for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sv.locate(batch, &shard, &first, &count);
+        uint32_t rec = first + (uint32_t)(lane >> 2);
+        const bool valid = rec < count;
+        if (!valid) rec = first;
+        const size_t ri = (size_t)shard * p.vShardCap + rec;
+        const VertexKey K = p.vk[ri];
+        const EdgeSeg E = edge_segment(p, K.w, K.vidKey >> 16);
+        // the root: lane j of the quad walks edge sample j (vertex_body, 16 per wave)
+        const float sx = edge_sample(E.e[0], E.d[0], qj);
+        const float sy = edge_sample(E.e[1], E.d[1], qj);
+        const float sz = edge_sample(E.e[2], E.d[2], qj);
+        CullMask cmv{0ull, 0ull};
+        if (p.cull) cmv = cull_mask_mpus(p, K.w);
+        float fv;
+        if (p.debug & 256u) fv = sx;  // ablation bit 8: no phase-A walk
+        else fv = ev.template eval<4, false>(sx, sy, sz, cmv, nullptr);
+        const float fs0 = quad_bcast<0>(fv), fs1 = quad_bcast<1>(fv), fs2 = quad_bcast<2>(fv), fs3 = quad_bcast<3>(fv);
+        const bool st0 = fs0 >= 0.5f;
+        const int iv = ((fs1 >= 0.5f) != st0) ? 1 : (((fs2 >= 0.5f) != st0) ? 2 : 3);
+        const float fa = iv == 1 ? fs0 : (iv == 2 ? fs1 : fs2);
+        const float fb = iv == 1 ? fs1 : (iv == 2 ? fs2 : fs3);
+        const float scale = (0.5f - fa) / (fb - fa);
+        // value, colour and normal at the root (finish_body, 16 per wave)
+        float P[3];
+        vertex_root(E, (uint32_t)iv, scale, P);
+        const bool onSeg = scale >= 0.0f && scale <= 1.0f;
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        if (!(p.debug & 32u)) {  // ablation bit 5: no walks
+            CullMask cm{0ull, 0ull};
+            if (p.cull) {
+                if (ballot(!onSeg) == 0ull) cm = cmv;  // cull_mask_mpus(p, K.w), as just made
+                else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
+            }
+            const float qx = qj == 1 ? P[0] + delta : P[0];
+            const float qy = qj == 2 ? P[1] + delta : P[1];
+            const float qz = qj == 3 ? P[2] + delta : P[2];
+            float c4[3];
+            const float g = ev.template eval<1, true>(qx, qy, qz, cm, c4);
+            c[0] = quad_bcast<0>(c4[0]);
+            c[1] = quad_bcast<0>(c4[1]);
+            c[2] = quad_bcast<0>(c4[2]);
+            const float vtx = quad_bcast<0>(g);
+            nx = (quad_bcast<1>(g) - vtx) * inv;
+            ny = (quad_bcast<2>(g) - vtx) * inv;
+            nz = (quad_bcast<3>(g) - vtx) * inv;
+            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);
+            nx = nx * im;
+            ny = ny * im;
+            nz = nz * im;
+        }
+        if (!scanSeen) {
+            surface_wait_scan(p);
+            scanSeen = true;
+        }
+        const uint32_t gi = (uint32_t)surface_offs(p, K.w) + (K.vidKey & 0xffffu);
+        if (valid && qj < 3 && gi < p.vCap) {  // past vCap: finish() grows and re-runs
+            const uint32_t o = gi * 3 + (uint32_t)qj;
+            p.pos[o] = qj == 0 ? P[0] : (qj == 1 ? P[1] : P[2]);
+            p.nrm[o] = qj == 0 ? nx : (qj == 1 ? ny : nz);
+            p.col[o] = qj == 0 ? c[0] : (qj == 1 ? c[1] : c[2]);
+        }
+    }
+    if (p.debug & 64u) return;  // ablation bit 6: no triangles
+    const ShardBatches sb(sCnt + kShards, p.tShardCap, 64);
+    if (wave0 < sb.total && !scanSeen) surface_wait_scan(p);
+    for (uint32_t batch = wave0; batch < sb.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sb.locate(batch, &shard, &first, &count);
+        const uint32_t t = first + lane;
+        if (t >= count) continue;
+        const TriRec R = p.tq[(size_t)shard * p.tShardCap + t];
+        const uint64_t o = surface_offs(p, ((R.a >> 12) << 6) | shard);  // the record's shard is w & 63
+        const uint32_t gt = (uint32_t)(o >> 32) + (R.a & 2047u);
+        const uint32_t base = (uint32_t)o;
+        if (gt >= p.tCap) continue;  // finish() grows and re-runs
+        p.tris[gt * 3 + 0] = base + (R.b & 2047u);
+        p.tris[gt * 3 + 1] = base + ((R.b >> 11) & 2047u);
+        p.tris[gt * 3 + 2] = base + ((R.b >> 22) | (((R.a >> 11) & 1u) << 10));
+    }
+}
+
 // Field probe for tests: mode 0 quads of consecutive points, 1 per point, 2 + colour.
 template <class EV>
 __device__ __forceinline__ void probe_body(const Params& p, float* lds, const float* xyz, float* out, float* colOut,

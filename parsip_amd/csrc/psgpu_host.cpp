@@ -568,6 +568,14 @@ int vertex_vpw(const psgpu_ctx* c) {
     return (uint64_t)c->lastV > 16u * waves && !c->alone ? 64 : 16;  // a lone run: the quad
 }
 
+// k_vertex + k_finish as one launch (k_surface) for the next run: 1 forces it, 2 (default) when
+// both would take their quad layouts (a launch too small to fill the device: its step is the
+// launch floor); only with the small-launch kernels (compiled with the split)
+bool use_surface(const psgpu_ctx* c) {
+    if (!c->jit || !c->jit->surface || c->fusedSurface == 0) return false;
+    return c->fusedSurface == 1 || (vertex_vpw(c) == 16 && finish_vpw(c) == 16 && c->lastV != 0);
+}
+
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
@@ -593,6 +601,19 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
         const uint64_t vv = (uint64_t)c->lastV + c->lastV / 8 + 256;
         gridV = std::max(p.scanBlocks, std::min<uint32_t>(gridV, (uint32_t)((vv + 4ull * vpwV - 1) / (4ull * vpwV))));
         gridF = std::min<uint32_t>(gridF, (uint32_t)((vv + 4ull * vpw - 1) / (4ull * vpw)));
+    }
+    if (use_surface(c)) {  // both quad layouts in one launch: the vertex grid (16 per wave)
+        uint32_t gridS = std::max(persistV, p.scanBlocks);
+        if (c->gridFit && c->lastV) {
+            const uint64_t vv = (uint64_t)c->lastV + c->lastV / 8 + 256;
+            gridS = std::max(p.scanBlocks, std::min<uint32_t>(gridS, (uint32_t)((vv + 63ull) / 64ull)));
+        }
+        PSGPU_CHECK(launch_jit(J->surface, gridS, 256, 0, s, p));
+        if (timed) {
+            PSGPU_CHECK(hipEventRecord(c->ev[3], s));
+            PSGPU_CHECK(hipEventRecord(c->ev[4], s));
+        }
+        return PSGPU_RET_SUCCESS;
     }
     if (J) PSGPU_CHECK(launch_jit(vpwV == 64 ? J->vertexW : J->vertex, gridV, 256, 0, s, p));
     else PSGPU_CHECK(launch_vertex(p, s, gridV));
@@ -643,7 +664,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
     const uint32_t shape[6] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
-                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c), use_split(c) ? 1u : 0u};
+                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c), (use_split(c) ? 1u : 0u) | (use_surface(c) ? 2u : 0u)};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
           memcmp(g.shape, shape, sizeof(shape)) == 0)) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -992,6 +1013,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (const char* e = getenv("PSGPU_FINISH_QUAD")) c->finishQuad = std::min(3, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_VERTEX_WIDE")) c->vertexWide = std::min(2, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_MPU_MARGIN")) c->mpuMarginDiv = std::max(1, atoi(e));
+    if (const char* e = getenv("PSGPU_FUSED_SURFACE")) c->fusedSurface = std::min(2, std::max(0, atoi(e)));
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -1068,6 +1090,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         }
     }
     else if (option == PSGPU_OPT_SPLIT_MAX_QUEUED && value >= 0 && value <= 0xffffffffll) c->splitMaxQueued = (uint32_t)value;
+    else if (option == PSGPU_OPT_FUSED_SURFACE && value >= 0 && value <= 2) c->fusedSurface = (int)value;
     else if (option == PSGPU_OPT_TIER_RUNS && value >= 1 && value <= (1 << 30)) c->tierRuns = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 3) return PSGPU_RET_PARAM_ERROR;
@@ -1103,7 +1126,9 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         c->stampCap = 0;
         drop_graphs(c);
         if (value > 0) {
-            PSGPU_CHECK(hipMalloc(&c->stamps, (size_t)kNumStampKernels * value * 24 + (size_t)value * 64));
+            const size_t bytes = (size_t)kNumStampKernels * value * 24 + (size_t)value * 64;
+            PSGPU_CHECK(hipMalloc(&c->stamps, bytes));
+            PSGPU_CHECK(hipMemset(c->stamps, 0, bytes));  // a kernel a run does not launch leaves no rows
             c->stampCap = (uint32_t)value;
         }
     }

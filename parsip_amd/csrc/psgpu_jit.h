@@ -16,6 +16,7 @@ struct JitKernels {
     hipFunction_t precheck = nullptr, mpu = nullptr, vertex = nullptr, vertexW = nullptr, finish = nullptr,
                   finishQ = nullptr, finishP = nullptr, probe = nullptr;
     hipFunction_t precheckS = nullptr, mpuS = nullptr;  // tree split at the root (two waves per item)
+    hipFunction_t surface = nullptr;  // k_vertex + k_finish in one launch (small launches; with the split kernels)
 };
 
 extern const char* const kJitArch;  // "gfx950"

@@ -178,8 +178,10 @@ struct ShardCtr {           // one 128-B line per shard: atomics on one line ser
 };
 struct DevCounters {
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
-    uint32_t error;          // protocol errors (bit 0: offsets-scan look-back timeout)
-    uint32_t pad[30];
+    uint32_t error;          // protocol errors (bit 0: offsets-scan look-back timeout, bit 1: k_surface's
+                             // wait for the scan timed out)
+    uint32_t scanDone;       // k_surface: offsets-scan blocks finished (released) in this run
+    uint32_t pad[29];
     ShardCtr shard[kShards];
 };
 

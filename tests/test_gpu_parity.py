@@ -141,6 +141,46 @@ def test_tree_split_golden(gpu_poly, name):
         assert seen[0] == digs[name]
 
 
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_fused_surface_golden(gpu_poly, name):
+    """k_vertex + k_finish as one launch (OPT_FUSED_SURFACE 1; the small-launch kernels compile
+    with OPT_TREE_SPLIT) reproduce the committed oracle digests; on a 1/8 cost share the
+    automatic choice (2) takes the fused kernel from the second run on (no k_vertex waves in the
+    timeline) and equals the two-kernel run."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
+    model, cs, _ = synth.make_config(name)
+    gpu_poly.set_model(model)
+
+    def digest():
+        gm, gs = gpu_poly.download(), gpu_poly.stats()
+        st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+        return mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris())
+    try:
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 1)
+        gpu_poly.jit_wait()  # the split option compiles the small-launch kernels
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 1)
+        for _ in range(2):
+            gpu_poly.run(cs)
+            assert digest() == dig
+        b = gpu_poly.plan_split(cs, 8)
+        lo, hi = int(b[3]), int(b[4])
+        got = {}
+        for mode in (0, 2):
+            gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, mode)
+            gpu_poly.run(cs, lo, hi)
+            gpu_poly.set_option(gpu.OPT_STAMPS, 1 << 15)
+            gpu_poly.run(cs, lo, hi)
+            vertex_waves = len(gpu_poly.stamps()["k_vertex"])
+            gpu_poly.set_option(gpu.OPT_STAMPS, 0)
+            got[mode] = digest()
+            assert (vertex_waves == 0) == (mode == 2), (mode, vertex_waves)
+        assert got[0] == got[2] and got[0]["vertices"] > 0
+    finally:
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
+
+
 def test_engines_pipelined_c3_golden():
     """The bench's pipelining: 4 contexts take 12 C3 polygonizations in turn, queued without
     host synchronisation (bench.py's timed loop); every context's last mesh equals the

@@ -157,10 +157,13 @@ def test_generated_kernels_resources():
 
     ks = kr.compile_variant("C3", 1 | 4, {})
     floor = {"jit_precheck": 7, "jit_mpu": 6, "jit_vertex": 8, "jit_vertex_w": 8, "jit_finish": 7,
-             "jit_finish_p": 7, "jit_finish_q": 6, "jit_precheck_s": 7, "jit_mpu_s": 7}
+             "jit_finish_p": 7, "jit_finish_q": 6, "jit_precheck_s": 7, "jit_mpu_s": 7, "jit_surface": 6}
     for name, want in floor.items():
         r = ks[name]
-        assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["sgpr_spill"] == 0, (name, r)
+        # k_surface (two walks in one kernel) sits at the SGPR ceiling and spills a few SGPRs
+        # into VGPR lanes (v_writelane / v_readlane, no scratch); it was measured with them
+        sgpr_ok = r["sgpr_spill"] <= (16 if name == "jit_surface" else 0)
+        assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and sgpr_ok, (name, r)
         assert r["waves_per_simd"] >= want, (name, r["waves_per_simd"], r["limited_by"], r["vgpr"], r["sgpr"])
 
 

@@ -33,7 +33,8 @@ MPU_S_DYNAMIC_LDS = 2 * K_LDS_MPU  # the tree-split k_mpu: 2 MPUs per block
 ROLE = {"jit_precheck": "k_precheck", "jit_mpu": "k_mpu", "jit_vertex": "k_vertex (quad, 16/wave)",
         "jit_vertex_w": "k_vertex (wide, 64/wave)", "jit_finish": "k_finish (64/wave)",
         "jit_finish_q": "k_finish (quad, 16/wave)", "jit_finish_p": "k_finish (pair, 32/wave)",
-        "jit_precheck_s": "k_precheck (tree split)", "jit_mpu_s": "k_mpu (tree split)", "jit_probe": "probe"}
+        "jit_precheck_s": "k_precheck (tree split)", "jit_mpu_s": "k_mpu (tree split)",
+        "jit_surface": "k_vertex + k_finish in one launch (small launches, quad layouts)", "jit_probe": "probe"}
 
 
 def parse_metadata(co: str) -> dict:
