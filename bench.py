@@ -876,6 +876,9 @@ def main():
                            "alternate between the engines and are queued without host sync",
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
                    "exchange": exchange, "culling": not args.no_cull, "tree_split": args.tree_split,
+                   "fused_surface": ("auto: k_vertex + k_finish as one launch when both take their quad layouts"
+                                     if args.tree_split and os.environ.get("PSGPU_FUSED_SURFACE", "2") != "0"
+                                     else "off"),
                    "kernels": kernels_label, "tiers": tiers_timed, "set_model_s": round(t_model, 4),
                    "jit_ready_s": round(t_jit, 3),
                    "host_enqueue_ms": round((t_enq - t0) * 1e3, 4)},
