@@ -338,9 +338,6 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        run's vertices take the quad layouts in both (small rank
                                        shares), 1 always, 0 never.  Needs the small-launch kernels,
                                        compiled with PSGPU_OPT_TREE_SPLIT != 0.  Identical output */
-#define PSGPU_OPT_FUSED_FRONT 22    /* k_precheck + k_mpu as one launch (the S1 queue released inside
-                                       it, a grid barrier before S2) for runs that take the tree
-                                       split: 1 or 2; 0 (default) two launches.  Identical output */
 #define PSGPU_OPT_MPU_TICKS    19   /* 1: runs record per-MPU ticks for MPUSTATS
                                        (psgpu_download_process_stats); 0 (default) off */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the

@@ -829,7 +829,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wav
 // (combine / bound_combine): the same values, half the walk per wave -- for launches whose
 // span is the heaviest brick's walk (small rank shares, a single engine).  Every wave of the
 // block reaches both barriers; the second wave of a brick stops after them.
-template <class EV, int SPLIT = 1, bool FRONT = false>
+template <class EV, int SPLIT = 1>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = wave_index();
     const int lane = lane_id();
@@ -990,8 +990,7 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     base = lane_value(base, 0);
     if (pass) {
         const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
-        if constexpr (FRONT) __hip_atomic_store(&p.pq[slotq], mOf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else p.pq[slotq] = mOf;
+        p.pq[slotq] = mOf;
         // the MPU's octants proven uniform by the same bounds: k_mpu evaluates only the others
         // (their inside bits are the proof's), bits 0-7 all outside, 8-15 all inside
         if (PSGPU_S2_OCT)
@@ -1014,23 +1013,12 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
             const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << q) - 1u));
             const uint32_t wq = lane_value(mOf, q) - p.mpuBegin;
             if (lane == 0) {
-                if constexpr (FRONT) {  // agent-coherent (write-through) stores: read in this launch
-                    __hip_atomic_store(&p.pqMask[2 * slotq], g.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&p.pqMask[2 * slotq + 1], g.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    p.pqMask[2 * slotq] = g.lo;
-                    p.pqMask[2 * slotq + 1] = g.hi;
-                }
+                p.pqMask[2 * slotq] = g.lo;
+                p.pqMask[2 * slotq + 1] = g.hi;
                 p.mpuMasks[2 * wq] = g.lo;
                 p.mpuMasks[2 * wq + 1] = g.hi;
             }
         }
-    }
-    // k_front: this wave's queue entries (pq, pqMask) written back for the S2 blocks of the
-    // same launch on other XCDs (only waves that queued reach this point)
-    if constexpr (FRONT) {
-        if (p.debug & (1u << 25)) __builtin_amdgcn_s_waitcnt(0);  // bit 25 (A/B): entries acknowledged, no L2 write-back
-        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
 }
 
@@ -1161,15 +1149,7 @@ __device__ __forceinline__ void s2_octants(const EV& ev, const float o[3], float
 // SPLIT 2 (tree split): two waves per MPU, each walking one subtree of the root over all
 // 8 x-slices (evaln_part), the values exchanged through LDS and combined by both waves
 // (combine), which then share the record passes as the W > 1 x-slice split does.
-// A word of the S1 queue: k_front's S2 blocks read entries written in the same launch with
-// agent-scope loads (past the non-coherent caches; no acquire: DESIGN.md §5), k_mpu plainly.
-template <bool FRONT, class T>
-__device__ __forceinline__ T queue_load(const T* q) {
-    if constexpr (FRONT) return __hip_atomic_load(const_cast<T*>(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *q;
-}
-
-template <class EV, int SPLIT = 1, bool FRONT = false>
+template <class EV, int SPLIT = 1>
 __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, uint32_t* item) {
     *item = 0xffffffffu;
     constexpr int WPM = SPLIT > 1 ? SPLIT : kMpuWaves;  // waves per MPU
@@ -1183,15 +1163,14 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // the 64 shard queues: lane s holds shard s's count); the grid is sized by the host
     // from the last finished run, and a run with more survivors than that is re-run by finish()
     phase_stamp(p, 0);
-    const uint32_t blk = FRONT ? blockIdx.x - p.preBlocks : blockIdx.x;  // k_front: S2 blocks follow the S1 ones
-    const uint32_t d = blk * (uint32_t)MPB + (uint32_t)slot;
+    const uint32_t d = blockIdx.x * (uint32_t)MPB + (uint32_t)slot;
     ModelPtr M = as_const(p.model);
     const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident (an LDS copy per block measured slower, r05)
     // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
     // the block
     __shared__ uint32_t sIncl[kShards];
     if (wave == 0) {
-        const uint32_t cnt = queue_load<FRONT>(&p.ctr->shard[lane].p);  // kShards == 64: one shard per lane
+        const uint32_t cnt = p.ctr->shard[lane].p;  // kShards == 64: one shard per lane
         sIncl[lane] = wave_incl_scan(cnt);
     }
     __syncthreads();
@@ -1200,7 +1179,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // a run with more survivors than that is re-run by finish()
     const uint32_t incl = sIncl[lane];
     const uint32_t pcount = sIncl[kShards - 1];
-    if (blk * (uint32_t)MPB >= pcount) return;  // whole block past the last survivor
+    if (blockIdx.x * (uint32_t)MPB >= pcount) return;  // whole block past the last survivor
     const bool live = d < pcount;
     uint32_t m = 0, w = 0;
     float o[3] = {0.0f, 0.0f, 0.0f};
@@ -1211,15 +1190,15 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
         const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
         const uint32_t slotq = uniform(pshard * p.pShardCap + pidx);
-        m = uniform(queue_load<FRONT>(&p.pq[slotq]));
+        m = uniform(p.pq[slotq]);
         if (p.cull) {  // the MPU box's culling mask, made by k_precheck: in SGPRs, so every
                        // per-primitive culling test of the walk is a scalar branch
 #if PSGPU_UNIFORM_CM
-            cm.lo = uniform64(queue_load<FRONT>(&p.pqMask[2 * slotq]));
-            cm.hi = uniform64(queue_load<FRONT>(&p.pqMask[2 * slotq + 1]));
+            cm.lo = uniform64(p.pqMask[2 * slotq]);
+            cm.hi = uniform64(p.pqMask[2 * slotq + 1]);
 #else
-            cm.lo = queue_load<FRONT>(&p.pqMask[2 * slotq]);
-            cm.hi = queue_load<FRONT>(&p.pqMask[2 * slotq + 1]);
+            cm.lo = p.pqMask[2 * slotq];
+            cm.hi = p.pqMask[2 * slotq + 1];
 #endif
         }
         if (PSGPU_S2_OCT) oct = uniform((uint32_t)p.pqOct[slotq]);
@@ -2152,48 +2131,6 @@ __device__ __forceinline__ void surface_wait_scan(const Params& p) {
 // an offsets word written by this launch's scan blocks (released before their scanDone count)
 __device__ __forceinline__ uint64_t surface_offs(const Params& p, uint32_t i) {
     return __hip_atomic_load(&p.offs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// k_front (PSGPU_OPT_FUSED_FRONT): k_precheck and k_mpu (tree split) in one launch for small
-// launches.  Blocks [0, preBlocks) are k_precheck's (S1 + bounds; a wave that queued survivors
-// releases its entries, then thread 0 counts the block done in shard b % 64, and the block
-// that completes a shard counts the shard in frontDone: atomics on one address serialise, a
-// count per block there cost ~30 us per launch); the blocks after them are k_mpu's, mapped
-// to queued survivors as k_mpu maps its blocks, and start once every shard is counted (a grid
-// barrier, bounded: a broken protocol flags error bit 2 instead of hanging).  The S1 blocks have the lowest ids, so each XCD dispatches all of its S1 blocks
-// before any waiting S2 block: the wait cannot starve them.  Same values as the two kernels.
-__device__ __forceinline__ void front_wait(const Params& p) {
-    if (lane_id() == 0) {
-        uint32_t spins = 0;
-        const uint32_t shards = min(p.preBlocks, (uint32_t)kShards);
-        while (__hip_atomic_load(&p.ctr->frontDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shards) {
-            if (p.debug & (1u << 26)) __builtin_amdgcn_s_sleep(60);  // timing experiment: slower polling
-            else __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 22)) {
-                atomicOr(&p.ctr->error, 4u);
-                break;
-            }
-        }
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // queue reads follow (queue_load<true>)
-}
-template <class EV>
-__device__ __forceinline__ void front_body(const Params& p, unsigned char* smem, uint32_t* item) {
-    if (blockIdx.x < p.preBlocks) {  // block-uniform
-        *item = 0xffffffffu;
-        precheck_body<EV, 2, true>(p, reinterpret_cast<float*>(smem));
-        __syncthreads();  // every wave of the block has released what it queued
-        if (threadIdx.x == 0 && !(p.debug & (1u << 27))) {  // bit 27: timing experiment only (no barrier)
-            const uint32_t s = blockIdx.x & (kShards - 1);
-            const uint32_t n = p.preBlocks / kShards + (s < p.preBlocks % kShards ? 1u : 0u);  // the shard's blocks
-            if (__hip_atomic_fetch_add(&p.ctr->shard[s].f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1u)
-                __hip_atomic_fetch_add(&p.ctr->frontDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    if (threadIdx.x < 64 && !(p.debug & (1u << 27))) front_wait(p);
-    __syncthreads();
-    mpu_body<EV, 2, true>(p, smem, item);
 }
 
 // k_surface (PSGPU_OPT_FUSED_SURFACE): k_vertex and k_finish in one launch for small launches

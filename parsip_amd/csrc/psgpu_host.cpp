@@ -576,12 +576,6 @@ bool use_surface(const psgpu_ctx* c) {
     return c->fusedSurface == 1 || (vertex_vpw(c) == 16 && finish_vpw(c) == 16 && c->lastV != 0);
 }
 
-// k_precheck + k_mpu as one launch (k_front) for the next run: with the tree split (a launch
-// too small to fill the device), 1 or 2 (auto) -- 0 keeps the two launches
-bool use_front(const psgpu_ctx* c) {
-    return c->fusedFront != 0 && c->jit && c->jit->front && use_split(c);
-}
-
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     Params p = pin;
     const uint32_t persistV = (uint32_t)(c->numCUs * c->vertexBlocksPerCU);
@@ -590,13 +584,6 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     JitKernels* J = c->jit.get();
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     const bool split = use_split(c);
-    if (use_front(c)) {  // S1 blocks, then S2 blocks (k_mpu's grid and LDS) in one launch
-        PSGPU_CHECK(launch_jit(J->front, p.preBlocks + p.mpuBlocks, 256, mpu_lds_bytes(0) / 2, s, p));
-        if (timed) {
-            PSGPU_CHECK(hipEventRecord(c->ev[1], s));
-            PSGPU_CHECK(hipEventRecord(c->ev[2], s));
-        }
-    } else {
     if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
@@ -604,7 +591,6 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0) / (split ? 2 : 1), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
-    }
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
     const int vpwV = J ? vertex_vpw(c) : 16;
     uint32_t gridV = std::max(persistV, p.scanBlocks);
@@ -678,8 +664,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
     const uint32_t shape[6] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
-                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c), (use_split(c) ? 1u : 0u) | (use_surface(c) ? 2u : 0u) |
-                               (use_front(c) ? 4u : 0u)};
+                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c), (use_split(c) ? 1u : 0u) | (use_surface(c) ? 2u : 0u)};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
           memcmp(g.shape, shape, sizeof(shape)) == 0)) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -1029,7 +1014,6 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (const char* e = getenv("PSGPU_VERTEX_WIDE")) c->vertexWide = std::min(2, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_MPU_MARGIN")) c->mpuMarginDiv = std::max(1, atoi(e));
     if (const char* e = getenv("PSGPU_FUSED_SURFACE")) c->fusedSurface = std::min(2, std::max(0, atoi(e)));
-    if (const char* e = getenv("PSGPU_FUSED_FRONT")) c->fusedFront = std::min(2, std::max(0, atoi(e)));
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -1107,7 +1091,6 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     }
     else if (option == PSGPU_OPT_SPLIT_MAX_QUEUED && value >= 0 && value <= 0xffffffffll) c->splitMaxQueued = (uint32_t)value;
     else if (option == PSGPU_OPT_FUSED_SURFACE && value >= 0 && value <= 2) c->fusedSurface = (int)value;
-    else if (option == PSGPU_OPT_FUSED_FRONT && value >= 0 && value <= 2) c->fusedFront = (int)value;
     else if (option == PSGPU_OPT_TIER_RUNS && value >= 1 && value <= (1 << 30)) c->tierRuns = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 3) return PSGPU_RET_PARAM_ERROR;

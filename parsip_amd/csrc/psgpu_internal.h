@@ -69,7 +69,6 @@ struct psgpu_ctx {
     int finishQuad = 2;  // PSGPU_OPT_FINISH_QUAD: 0 one lane, 1 a quad, 3 a pair of lanes per vertex, 2 by the last run's vertex count
     int treeSplit = 0;   // PSGPU_OPT_TREE_SPLIT: 1 k_precheck / k_mpu walk the root's two subtrees in two waves
     bool splittable = false;  // the model's walk splits at the root (jit_splittable)
-    int fusedFront = 0;       // PSGPU_OPT_FUSED_FRONT: k_precheck + k_mpu in one launch (use_front)
     int fusedSurface = 2;     // PSGPU_OPT_FUSED_SURFACE: k_vertex + k_finish in one launch (use_surface)
     uint32_t splitMaxQueued = 1024;  // PSGPU_OPT_SPLIT_MAX_QUEUED: tree split 2 applies up to this many S2 MPUs
                                      // (psgpu_create: 4 per CU; C3's 1/8 shares queue ~800, 1/4 ~1,600)

@@ -17,7 +17,6 @@ struct JitKernels {
                   finishQ = nullptr, finishP = nullptr, probe = nullptr;
     hipFunction_t precheckS = nullptr, mpuS = nullptr;  // tree split at the root (two waves per item)
     hipFunction_t surface = nullptr;  // k_vertex + k_finish in one launch (small launches; with the split kernels)
-    hipFunction_t front = nullptr;    // k_precheck + k_mpu (tree split) in one launch (small launches)
 };
 
 extern const char* const kJitArch;  // "gfx950"

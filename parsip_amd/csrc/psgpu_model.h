@@ -174,16 +174,14 @@ struct ShardCtr {           // one 128-B line per shard: atomics on one line ser
     uint32_t t;             // triangle records appended
     uint32_t s;             // surface MPUs (>= 1 triangle)
     uint32_t b;             // S1 survivors proven empty by field bounds (not queued)
-    uint32_t f;             // k_front: S1 blocks b with b % 64 == shard finished
-    uint32_t pad[26];
+    uint32_t pad[27];
 };
 struct DevCounters {
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
     uint32_t error;          // protocol errors (bit 0: offsets-scan look-back timeout, bit 1: k_surface's
-                             // wait for the scan timed out, bit 2: k_front's wait for its S1 blocks)
+                             // wait for the scan timed out)
     uint32_t scanDone;       // k_surface: offsets-scan blocks finished (released) in this run
-    uint32_t frontDone;      // k_front: shards whose S1 blocks all finished (ShardCtr::f) in this run
-    uint32_t pad[28];
+    uint32_t pad[29];
     ShardCtr shard[kShards];
 };
 

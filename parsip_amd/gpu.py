@@ -85,7 +85,6 @@ OPT_SPLIT_MAX_QUEUED = 17
 OPT_TIER_RUNS = 18
 OPT_MPU_TICKS = 19
 OPT_FUSED_SURFACE = 21
-OPT_FUSED_FRONT = 22
 DEBUG_EXPORT_POISON = 1 << 23  # test hooks of the blocking export (OPT_DEBUG bits)
 DEBUG_EXPORT_STRAGGLER = 1 << 24
 JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values
