@@ -263,6 +263,22 @@ int  psgpu_download_process_stats(psgpu_ctx* ctx, PsMpuProcessStats* out);
  * XCC_ID << 16.  Unlaunched waves read zero; then cap x 8 words of k_mpu phase stamps
  * (PSGPU_OPT_DEBUG bit 4096; profiling only).  Pass out = NULL to query *cap. */
 int  psgpu_download_stamps(psgpu_ctx* ctx, uint64_t* out, uint32_t* cap);
+/* PrintThreadResults (PS_Polygonizer.h:393, body .cpp:414-428, counters .cpp:443-469).
+ * The reference keeps one (processed, crossed) MPU count pair per TBB worker that ran an
+ * MPU, accumulated over every Polygonize of the process.  Here the worker is a device
+ * context: every finished run (psgpu_finish, and every call built on it: the blocking
+ * psgpu_polygonize_mpus, group parts, comm ranks) adds the MPUs of its range and those with
+ * ctTriangles > 0 to its context's entry; entries are enumerated in the order contexts first
+ * finished a run and outlive their context.  This divides each entry by ctAttempts, stores
+ * entry i into lpThreadProcessed[i] / lpThreadCrossed[i] (either may be NULL; at most
+ * `capacity` entries are written: pass psgpu_thread_result_count()), prints
+ * "Thread#  i, Processed MPUs p, Crossed MPUs c " lines as the reference when print != 0,
+ * clears every entry, and returns the number of entries.  ctAttempts <= 0:
+ * PSGPU_RET_PARAM_ERROR, nothing cleared. */
+int  psgpu_print_thread_results(int ctAttempts, uint32_t* lpThreadProcessed, uint32_t* lpThreadCrossed,
+                                uint32_t capacity, int print);
+/* Entries psgpu_print_thread_results would report now. */
+int  psgpu_thread_result_count(void);
 /* Device-side timing of the last polygonize, per kernel (ms); returns count filled. */
 int  psgpu_last_kernel_times(psgpu_ctx* ctx, float* ms, int maxKernels, const char** names);
 /* FieldComputer::fieldValue / fieldValueAndColor on n host points (xyz interleaved):
@@ -283,7 +299,13 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        bits 23 / 24 (test hooks of the blocking export): the
                                        staging past the piece flags is filled with the call's
                                        epoch before the export / the packing kernel's last
-                                       block waits ~40 us before each piece */
+                                       block waits ~40 us before each piece;
+                                       bits 25 / 26 (test hooks, the next run only): k_surface's
+                                       scan blocks count themselves done ~40 us late and its
+                                       waves give up waiting after a few spins / every
+                                       offsets-scan look-back times out; either way finish
+                                       sees the protocol error and re-runs the polygonization
+                                       as k_vertex + k_finish (a second error: -6) */
 #define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU; once a
                                              run of the same range has finished, the grid is fitted
                                              to its vertices (+1/8) up to this (env PSGPU_GRID_FIT=0:

@@ -528,6 +528,13 @@ struct PolyMPUs {  /* PS_Polygonizer.h:196-198 */
 using psgpu::CountMPUNeeded;
 using psgpu::Polygonize;
 using psgpu::PrepareBBoxes;
+/* PrintThreadResults (PS_Polygonizer.h:393, .cpp:414-428): one entry per device context
+ * that ran a Polygonize since the last call (the library's worker; psgpu_print_thread_results
+ * in parsip_gpu.h).  As the reference, the arrays must hold one U32 per entry:
+ * psgpu_thread_result_count() says how many. */
+inline void PrintThreadResults(int ctAttempts, uint32_t* lpThreadProcessed = NULL, uint32_t* lpThreadCrossed = NULL) {
+    psgpu_print_thread_results(ctAttempts, lpThreadProcessed, lpThreadCrossed, 0xffffffffu, 1);
+}
 }  // namespace SIMDPOLY
 }  // namespace PS
 #endif

@@ -837,6 +837,12 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int slot = wave / SPLIT;  // the block's brick
     phase_stamp(p, 0, 8192u);
     const uint64_t tick0 = p.mpuTicks ? stamp_now() : 0ull;  // MPUSTATS tickStart
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the words k_surface only ever raises (its wait's timeout, from any wave, after block 0
+        // published the rest): cleared here, before any kernel of the run can raise them
+        p.hostCtr->surfaceErr = 0u;
+        p.totals[7] = 0u;
+    }
     EV ev(as_const(p.model), lds + wave * p.slotsPerLane * 64 + lane);
     CullLanes cl;  // loaded first: independent of everything below
     if (p.cull) cl = load_cull_lanes(as_const(p.model));
@@ -1550,6 +1556,7 @@ __device__ __forceinline__ void scan_counts_block(const Params& p, uint32_t b) {
                     do {
                         w = __hip_atomic_load(&p.scanStatus[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } while ((w >> 62) == 0ull && ++spins < (1u << 20));
+                    if (p.debug & (1u << 26)) w = 0ull;  // test hook: every look-back times out
                     if ((w >> 62) == 0ull) {
                         atomicOr(&p.ctr->error, 1u);
                         w = scan_word(2, 0u, 0u);
@@ -2108,15 +2115,20 @@ if constexpr (VPW == 16) {
 
 // k_surface's wait for the offsets scan (every scan block released its offsets), bounded: a
 // broken protocol flags the run (error bit 1) instead of hanging the device.
+// The flag reaches the host through words block 0 never overwrites (surfaceErr, raised with
+// a plain store; totals[7], raised atomically), so a timeout after block 0 published the
+// counters still fails the run, and psgpu_finish re-runs it as k_vertex + k_finish.
 __device__ __forceinline__ void surface_wait_scan(const Params& p) {
     if (lane_id() == 0) {
         uint32_t spins = 0;
+        // test hook (PSGPU_OPT_DEBUG bit 25): a bound far below the scan blocks' delay
+        const uint32_t bound = (p.debug & (1u << 25)) ? 4u : (1u << 22);
         while (__hip_atomic_load(&p.ctr->scanDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.scanBlocks) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 22)) {  // block 0 published the counters long before: flag
-                atomicOr(&p.ctr->error, 2u);  // the run's totals and the host copy as well
+            if (++spins > bound) {
+                atomicOr(&p.ctr->error, 2u);
                 atomicOr(&p.totals[7], 2u);
-                p.hostCtr->error = p.hostCtr->error | 2u;
+                p.hostCtr->surfaceErr = 2u;
                 __threadfence_system();
                 break;
             }
@@ -2156,14 +2168,24 @@ __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
         scan_counts_block(p, blockIdx.x);
         __syncthreads();  // the block's offsets stores are in L2
         if (threadIdx.x == 0) {
+            if (p.debug & (1u << 25)) {  // test hook: the scan blocks count themselves done ~40 us late
+                const uint64_t t0 = stamp_now();
+                while (stamp_now() - t0 < 4000u) __builtin_amdgcn_s_sleep(8);
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // ... and written back for the other XCDs
             __hip_atomic_fetch_add(&p.ctr->scanDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (blockIdx.x == 0) {  // k_finish's block-0 duties (finish_body)
+    if (blockIdx.x == 0) {  // k_finish's block-0 duties (finish_body), once every scan block is done:
+        // a look-back timeout of any scan block (error bit 0) is then in the counters it publishes
+        if (threadIdx.x < 64) surface_wait_scan(p);
+        __syncthreads();
+        const uint32_t err = __hip_atomic_load(&p.ctr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(p.ctr);
         uint32_t* dst = reinterpret_cast<uint32_t*>(p.hostCtr);
-        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) dst[i] = src[i];
+        constexpr uint32_t kErrWord = __builtin_offsetof(DevCounters, error) / 4, kSurfWord = __builtin_offsetof(DevCounters, surfaceErr) / 4;
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x)
+            if (i != kSurfWord) dst[i] = i == kErrWord ? err : src[i];
         __threadfence_system();
         uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
         for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
@@ -2173,9 +2195,9 @@ __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
             const uint32_t tv = wave_sum(sc.v), tt = wave_sum(sc.t), tp = wave_sum(sc.p), tb = wave_sum(sc.b),
                            ts = wave_sum(sc.s);
             if (threadIdx.x == 0) {
-                const uint32_t tot[8] = {p.mpuCount, tv, tt, tp + tb, ts, tp, (uint32_t)p.ctr->firstOverflow,
-                                         p.ctr->error};
-                for (int i = 0; i < 8; ++i) p.totals[i] = tot[i];
+                const uint32_t tot[7] = {p.mpuCount, tv, tt, tp + tb, ts, tp, (uint32_t)p.ctr->firstOverflow};
+                for (int i = 0; i < 7; ++i) p.totals[i] = tot[i];
+                if (err) atomicOr(&p.totals[7], err);  // raised, never stored: zeroed by k_precheck
             }
         }
     }
@@ -2183,7 +2205,7 @@ __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
     stage_shard_counts(p, 1, sCnt);            // ShardCtr::v
     stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
     __syncthreads();
-    bool scanSeen = false;
+    bool scanSeen = blockIdx.x == 0;  // block 0 waited above
     const ShardBatches sv(sCnt, p.vShardCap, 16);
     const int qj = lane & 3;
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {

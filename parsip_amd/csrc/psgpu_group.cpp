@@ -124,14 +124,19 @@ int plan(psgpu_group* g, float cs, uint32_t total) {
     g->bounds[0] = 0;
     if (a > 1 && total > 0) {
         std::vector<uint32_t> costs(total);
+        // planning runs are not the caller's polygonizations: PrintThreadResults skips them
+        g->parts[0]->countThreads = false;
         for (uint32_t b = 0; b < total;) {
             const uint32_t e = (uint32_t)std::min<uint64_t>(total, (uint64_t)b + plan_chunk_mpus());
             int rc = psgpu_polygonize(g->parts[0], cs, b, e, nullptr);
-            if (rc != PSGPU_RET_SUCCESS) return rc;
-            rc = psgpu_mpu_costs(g->parts[0], costs.data() + b);
-            if (rc != PSGPU_RET_SUCCESS) return rc;
+            if (rc == PSGPU_RET_SUCCESS) rc = psgpu_mpu_costs(g->parts[0], costs.data() + b);
+            if (rc != PSGPU_RET_SUCCESS) {
+                g->parts[0]->countThreads = true;
+                return rc;
+            }
             b = e;
         }
+        g->parts[0]->countThreads = true;
         const int rc = psgpu_split_costs(costs.data(), total, a, 0, g->bounds.data());
         if (rc != PSGPU_RET_SUCCESS) return rc;
     }
@@ -632,8 +637,9 @@ int psgpu_comm_exchange_group(psgpu_comm* m, psgpu_group* g) {
 // none waits for a collective the failed rank will not enter.
 // If even that cannot be prepared (the device cannot be made current, or the flag cannot be
 // copied to it), the rank still enters the all-reduce, from the constant 2 kept beside the flag
-// (no copy needed); should the collective itself fail to enqueue, the communicator is aborted
-// (ncclCommAbort) and unusable from then on -- psgpu_comm_destroy is all that is left to call.
+// (no copy needed); should the collective itself fail to enqueue (on this path or on the
+// normal one), the communicator is aborted (ncclCommAbort) and unusable from then on --
+// psgpu_comm_destroy is all that is left to call.
 int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut) {
     if (!m || !m->pending || !m->ctx || !m->comm) return PSGPU_RET_PARAM_ERROR;
     psgpu_ctx* c = m->ctx;
@@ -677,7 +683,11 @@ int psgpu_comm_result(psgpu_comm* m, PsMeshInfo* totalOut, PsGroupPart* partsOut
     if (hipMemcpyAsync(m->flag, m->hostFlag, sizeof(uint32_t), hipMemcpyHostToDevice, s) != hipSuccess)
         return enter_failed(local != PSGPU_RET_SUCCESS ? local : PSGPU_RET_DEVICE_ERROR);
     int rc = nccl_fail(ncclAllReduce(m->flag, m->flag, 1, ncclUint32, ncclMax, m->comm, s), "ncclAllReduce");
-    if (rc != PSGPU_RET_SUCCESS) return local != PSGPU_RET_SUCCESS ? local : rc;
+    if (rc != PSGPU_RET_SUCCESS) {  // the other ranks may be inside the all-reduce: abort it for them
+        (void)ncclCommAbort(m->comm);
+        m->comm = nullptr;
+        return local != PSGPU_RET_SUCCESS ? local : rc;
+    }
     PSGPU_CHECK(hipMemcpyAsync(m->hostFlag, m->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     PSGPU_CHECK(hipStreamSynchronize(s));
     if (local != PSGPU_RET_SUCCESS) return local;

@@ -434,12 +434,23 @@ size_t brick_count(const psgpu_ctx* c) {
     return (size_t)bd[0] * bd[1] * bd[2];
 }
 
+// The S2-by-octants experiment (PSGPU_S2_OCT, off by default, measured slower: DESIGN.md §4)
+// is compiled in only through PSGPU_JIT_FLAGS; its per-entry proof words exist only then.
+bool s2_oct_enabled() {
+    static const bool on = [] {
+        const char* f = getenv("PSGPU_JIT_FLAGS");
+        const char* d = f ? strstr(f, "PSGPU_S2_OCT=") : nullptr;
+        return d != nullptr && d[13] != '\0' && d[13] != '0';
+    }();
+    return on;
+}
+
 int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     const size_t n = std::max<uint32_t>(mpuCount, 1);
     c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
     PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->pqMask, c->capPqMask, (size_t)c->pShardCap * kShards * 2));
-    PSGPU_CHECK(grow(c->pqOct, c->capPqOct, (size_t)c->pShardCap * kShards));
+    if (s2_oct_enabled()) PSGPU_CHECK(grow(c->pqOct, c->capPqOct, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
     PSGPU_CHECK(grow(c->passed, c->capPassed, n));
     PSGPU_CHECK(grow(c->mpuMasks, c->capMasks, 2 * n));
@@ -572,7 +583,7 @@ int vertex_vpw(const psgpu_ctx* c) {
 // both would take their quad layouts (a launch too small to fill the device: its step is the
 // launch floor); only with the small-launch kernels (compiled with the split)
 bool use_surface(const psgpu_ctx* c) {
-    if (!c->jit || !c->jit->surface || c->fusedSurface == 0) return false;
+    if (!c->jit || !c->jit->surface || c->fusedSurface == 0 || c->surfaceOff) return false;
     return c->fusedSurface == 1 || (vertex_vpw(c) == 16 && finish_vpw(c) == 16 && c->lastV != 0);
 }
 
@@ -648,13 +659,14 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     const Params p = make_params(c);
     c->runTicks = p.mpuTicks != nullptr;
-    c->debug &= ~(1 << 20);  // the short-grid test hook applies to one run
+    c->debug &= ~((1 << 20) | (1 << 25) | (1 << 26));  // the short-grid / protocol test hooks apply to one run
     if (p.spans) c->spanNext++;
     c->runMpuBlocks = p.mpuBlocks;
     c->runMpb = use_split(c) ? 2u : (uint32_t)kMpusPerBlock;
     const uint32_t slot = c->parity;
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool timed = c->timing != 0;
+    c->runSurface = use_surface(c);
     if (c->stamps)  // waves that do not run leave no stale records
         PSGPU_CHECK(hipMemsetAsync(c->stamps, 0, (size_t)kNumStampKernels * c->stampCap * 24 + (size_t)c->stampCap * 64, s));
     if (!c->useGraph || timed || s == nullptr) {
@@ -700,6 +712,28 @@ void set_pending(psgpu_ctx* c, bool v) {
     if (c->pending == v) return;
     c->pending = v;
     g_pendingRuns[c->device & 63].fetch_add(v ? 1 : -1);
+}
+
+// PrintThreadResults' counters (PS_Polygonizer.cpp:15-18, :443-469): the reference keeps a
+// (processed, crossed) pair per TBB worker that ran any MPU, over every Polygonize of the
+// process, enumerated in the order the workers first ran one, and cleared by
+// PrintThreadResults (.cpp:414-428).  The library's worker is a device context (one stream,
+// one polygonization at a time): every finished run adds its range's MPUs and its MPUs with
+// at least one triangle to its context's entry; an entry outlives its context, as a TBB
+// worker's counter outlives the call that made it, until the next print clears them all.
+std::atomic<uint64_t> g_ctxSerial{0};
+std::mutex g_threadMu;
+std::vector<std::pair<uint64_t, std::pair<uint64_t, uint64_t>>> g_threadCounts;  // serial -> (processed, crossed)
+void thread_results_add(uint64_t serial, uint32_t processed, uint32_t crossed) {
+    if (processed == 0) return;  // a worker that ran no MPU has no entry (never called local())
+    std::lock_guard<std::mutex> lk(g_threadMu);
+    for (auto& e : g_threadCounts)
+        if (e.first == serial) {
+            e.second.first += processed;
+            e.second.second += crossed;
+            return;
+        }
+    g_threadCounts.push_back({serial, {processed, crossed}});
 }
 
 // Adopt the model's specialised kernels once their compile has finished (wait: block for
@@ -957,6 +991,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (deviceOrdinal < 0 || deviceOrdinal >= n) return PSGPU_RET_DEVICE_ERROR;
     psgpu_ctx* c = new psgpu_ctx();
     c->device = deviceOrdinal;
+    c->serial = ++g_ctxSerial;
     int rc = set_device(c);
     if (rc != PSGPU_RET_SUCCESS) { delete c; return rc; }
     hipDeviceProp_t prop;
@@ -1259,9 +1294,21 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             }
         }
         const DevCounters& h = *c->hostCtr;
-        if (c->mpuCount && h.error) {
-            fprintf(stderr, "psgpu: device protocol error 0x%x\n", h.error);
-            return PSGPU_RET_DEVICE_ERROR;
+        if (c->mpuCount && (h.error | h.surfaceErr)) {
+            // an in-kernel wait gave up (an offsets-scan look-back, or k_surface's wait for the
+            // scan): the run's offsets are not trusted.  Re-run it once as k_vertex + k_finish,
+            // the chain whose kernel boundaries order the scan; a second error fails the call.
+            fprintf(stderr, "psgpu: device protocol error 0x%x (%s): re-running as k_vertex + k_finish\n",
+                    h.error | h.surfaceErr, c->runSurface ? "k_surface" : "k_vertex");
+            c->surfaceOff = true;
+            rc = enqueue(c, c->runStream);
+            c->surfaceOff = false;
+            if (rc != PSGPU_RET_SUCCESS) return rc;
+            PSGPU_CHECK(hipStreamSynchronize(c->runStream));
+            if (h.error | h.surfaceErr) {
+                fprintf(stderr, "psgpu: device protocol error 0x%x\n", h.error | h.surfaceErr);
+                return PSGPU_RET_DEVICE_ERROR;
+            }
         }
         if (c->debug & (1 << 21)) {  // test hook: this finish fails as a protocol error would (one run)
             c->debug &= ~(1 << 21);
@@ -1286,6 +1333,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         I.ctFieldMPUs = c->mpuCount ? Q : 0;
         I.ctLaneEvals = 8ull * c->mpuCount + 512ull * I.ctFieldMPUs + 8ull * I.ctVertices;
         c->haveResult = true;
+        if (c->countThreads) thread_results_add(c->serial, I.ctMPUs, I.ctSurfaceMPUs);
     }
     if (!c->haveResult) return PSGPU_RET_PARAM_ERROR;
     if (info) *info = c->info;
@@ -1324,6 +1372,29 @@ int psgpu_download_spans(psgpu_ctx* c, uint64_t* out, uint32_t* runs) {
             out[(size_t)r * 2 * kNumStampKernels + 2 * k + 1] = hi;
         }
     return PSGPU_RET_SUCCESS;
+}
+
+int psgpu_thread_result_count(void) {
+    std::lock_guard<std::mutex> lk(g_threadMu);
+    return (int)g_threadCounts.size();
+}
+
+int psgpu_print_thread_results(int ctAttempts, uint32_t* lpThreadProcessed, uint32_t* lpThreadCrossed,
+                               uint32_t capacity, int print) {
+    if (ctAttempts <= 0) return PSGPU_RET_PARAM_ERROR;  // the reference divides by it
+    std::lock_guard<std::mutex> lk(g_threadMu);
+    const int n = (int)g_threadCounts.size();
+    for (int i = 0; i < n; ++i) {
+        // the reference's int pair divided by int (.cpp:421-424)
+        const uint32_t pr = (uint32_t)(g_threadCounts[i].second.first / (uint64_t)ctAttempts);
+        const uint32_t cr = (uint32_t)(g_threadCounts[i].second.second / (uint64_t)ctAttempts);
+        if (lpThreadProcessed && (uint32_t)i < capacity) lpThreadProcessed[i] = pr;
+        if (lpThreadCrossed && (uint32_t)i < capacity) lpThreadCrossed[i] = cr;
+        if (print) printf("Thread#  %d, Processed MPUs %d, Crossed MPUs %d \n", i + 1, (int)pr, (int)cr);
+    }
+    if (print) fflush(stdout);
+    g_threadCounts.clear();
+    return n;
 }
 
 int psgpu_last_kernel_times(psgpu_ctx* c, float* ms, int maxKernels, const char** names) {

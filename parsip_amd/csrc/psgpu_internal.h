@@ -36,6 +36,8 @@ struct psgpu_ctx {
     using CubeTablesDev = psgpu::CubeTablesDev;
     static constexpr int kNumKernels = psgpu::kNumKernels;
     int device = 0;
+    uint64_t serial = 0;  // process-unique id: this context's PrintThreadResults entry
+    bool countThreads = true;  // finished runs add to that entry (off for a group's planning runs)
     int numCUs = 256;
     hipStream_t stream = nullptr;
     PsSoaBlobPrims primsHost;  // bbox + counts of the current model
@@ -70,6 +72,8 @@ struct psgpu_ctx {
     int treeSplit = 0;   // PSGPU_OPT_TREE_SPLIT: 1 k_precheck / k_mpu walk the root's two subtrees in two waves
     bool splittable = false;  // the model's walk splits at the root (jit_splittable)
     int fusedSurface = 2;     // PSGPU_OPT_FUSED_SURFACE: k_vertex + k_finish in one launch (use_surface)
+    bool runSurface = false;  // the last enqueued run took k_surface
+    bool surfaceOff = false;  // while finish re-runs a run whose in-kernel wait gave up: the two kernels
     uint32_t splitMaxQueued = 1024;  // PSGPU_OPT_SPLIT_MAX_QUEUED: tree split 2 applies up to this many S2 MPUs
                                      // (psgpu_create: 4 per CU; C3's 1/8 shares queue ~800, 1/4 ~1,600)
     uint32_t runMpb = 0;      // k_mpu MPUs per block of the last enqueued run

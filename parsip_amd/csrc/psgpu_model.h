@@ -181,7 +181,10 @@ struct DevCounters {
     uint32_t error;          // protocol errors (bit 0: offsets-scan look-back timeout, bit 1: k_surface's
                              // wait for the scan timed out)
     uint32_t scanDone;       // k_surface: offsets-scan blocks finished (released) in this run
-    uint32_t pad[29];
+    uint32_t surfaceErr;     // host copy only: 2 once a k_surface wave's scan wait timed out (plain
+                             // stores of one value, so no read-modify-write over PCIe); zeroed by
+                             // k_precheck, never copied from the device counters by k_surface
+    uint32_t pad[28];
     ShardCtr shard[kShards];
 };
 

@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = [
     "psgpu_comm_unique_id", "psgpu_comm_create", "psgpu_comm_destroy", "psgpu_comm_exchange",
     "psgpu_comm_result", "psgpu_download_stamps", "psgpu_comm_exchange_group", "psgpu_download_spans",
     "psgpu_comm_reexchanged", "psgpu_polygonize_mpus_ex", "psgpu_download_process_stats",
+    "psgpu_print_thread_results", "psgpu_thread_result_count",
 ]
 
 OPT_KERNEL_TIMING = 1
@@ -85,6 +86,8 @@ OPT_SPLIT_MAX_QUEUED = 17
 OPT_TIER_RUNS = 18
 OPT_MPU_TICKS = 19
 OPT_FUSED_SURFACE = 21
+DEBUG_SURFACE_LATE_SCAN = 1 << 25  # test hooks of the in-kernel waits (OPT_DEBUG bits, one run each)
+DEBUG_LOOKBACK_TIMEOUT = 1 << 26
 DEBUG_EXPORT_POISON = 1 << 23  # test hooks of the blocking export (OPT_DEBUG bits)
 DEBUG_EXPORT_STRAGGLER = 1 << 24
 JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values
@@ -127,6 +130,8 @@ def load(build_if_missing: bool = True):
         "psgpu_polygonize_mpus_ex": ([vp, f32, vp, vp, vp, vp, u32, ctypes.POINTER(u32), vp, vp], i32),
         "psgpu_download_process_stats": ([vp, vp], i32),
         "psgpu_last_kernel_times": ([vp, vp, i32, vp], i32),
+        "psgpu_print_thread_results": ([i32, vp, vp, u32, i32], i32),
+        "psgpu_thread_result_count": ([], i32),
         "psgpu_field_values": ([vp, vp, u32, i32, vp, vp], i32),
         "psgpu_set_option": ([vp, i32, ctypes.c_int64], i32),
         "psgpu_jit_active": ([vp], i32),
@@ -389,8 +394,16 @@ class Polygonizer:
             poly_mpus = np.zeros(soa.MAX_MPU_COUNT, soa.MPU_DTYPE)
         ct = ctypes.c_uint32()
         p, m, o = model.ptrs()
-        if process_stats is not None:
-            assert process_stats.dtype == soa.MPUSTATS_DTYPE and len(process_stats) >= len(poly_mpus)
+        # the library writes one record per MPU of the lattice (at most len(poly_mpus)): check
+        # the caller's arrays hold that many (a ValueError, not an assert: -O strips asserts)
+        need = min(len(poly_mpus), count_mpus(cellsize, *model.bbox))
+        for name, arr, dt in (("stats", stats, soa.MPU_STATS_DTYPE), ("process_stats", process_stats, soa.MPUSTATS_DTYPE)):
+            if arr is None:
+                continue
+            if arr.dtype != dt or not arr.flags.c_contiguous:
+                raise ValueError(f"{name}: a C-contiguous {dt} array is required")
+            if len(arr) < need:
+                raise ValueError(f"{name}: {len(arr)} records, the lattice needs {need}")
         rc = self._L.psgpu_polygonize_mpus_ex(self._ctx, cellsize, p, m, o, poly_mpus.ctypes.data, len(poly_mpus),
                                               ctypes.byref(ct), None if stats is None else stats.ctypes.data,
                                               None if process_stats is None else process_stats.ctypes.data)
@@ -446,6 +459,33 @@ class Polygonizer:
         _check(self._L.psgpu_field_values(self._ctx, xyz.ctypes.data, n, mode, out.ctypes.data, col.ctypes.data),
                "psgpu_field_values")
         return (out, col) if mode == 2 else out
+
+
+def PrintThreadResults(ct_attempts: int, processed: np.ndarray | None = None, crossed: np.ndarray | None = None,
+                       echo: bool = True) -> int:
+    """PS::SIMDPOLY::PrintThreadResults (PS_Polygonizer.h:393, .cpp:414-428): per worker (here a
+    device context, in the order contexts first finished a run since the last call) the MPUs
+    processed and those with ctTriangles > 0, summed over every polygonization of the process,
+    divided by ``ct_attempts``, written into ``processed`` / ``crossed`` (uint32 arrays, one
+    entry per worker: ``thread_result_count()``), printed as the reference prints them when
+    ``echo``, then cleared.  Returns the number of workers."""
+    L = load()
+    arrs = []
+    for a in (processed, crossed):
+        if a is not None and (a.dtype != np.uint32 or not a.flags.c_contiguous):
+            raise ValueError("processed / crossed: C-contiguous uint32 arrays are required")
+        arrs.append(a)
+    cap = min([len(a) for a in arrs if a is not None], default=0)
+    n = L.psgpu_print_thread_results(int(ct_attempts), None if processed is None else processed.ctypes.data,
+                                     None if crossed is None else crossed.ctypes.data, cap, int(echo))
+    if n < 0:
+        raise PsgpuError(n, "psgpu_print_thread_results")
+    return n
+
+
+def thread_result_count() -> int:
+    """Workers PrintThreadResults would report now."""
+    return int(load().psgpu_thread_result_count())
 
 
 _DEFAULT = {}

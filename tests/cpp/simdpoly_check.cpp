@@ -228,7 +228,7 @@ int main(int argc, char** argv) {
         o.write(reinterpret_cast<const char*>(tris.data()), (std::streamsize)(tris.size() * 4));
         return re == PSGPU_RET_SUCCESS ? 0 : 68;
     }
-    if ((mode == "soa" || mode == "soa-stats") && argc >= 5) {
+    if ((mode == "soa" || mode == "soa-stats" || mode == "soa-threads") && argc >= 5) {
         static PS::SIMDPOLY::SOABlobPrims prims;
         static PS::SIMDPOLY::SOABlobPrimMatrices mats;
         static PS::SIMDPOLY::SOABlobOps ops;
@@ -258,6 +258,26 @@ int main(int argc, char** argv) {
             put(o, t0);
             put(o, t1);
             o.write(reinterpret_cast<const char*>(stats.data()), (std::streamsize)poly->ctMPUs * sizeof(MPUSTATS));
+            return 0;
+        }
+        if (mode == "soa-threads") {  // Polygonize twice, then PrintThreadResults(2, ...) twice
+            const int rc1 = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *poly, NULL);
+            const int rc2 = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *poly);
+            const int n = psgpu_thread_result_count();
+            std::vector<uint32_t> pr(n > 0 ? n : 1, 0xdeadbeefu), cr(n > 0 ? n : 1, 0xdeadbeefu);
+            PS::SIMDPOLY::PrintThreadResults(2, pr.data(), cr.data());
+            const int after = psgpu_thread_result_count();
+            std::vector<uint32_t> pr2(4, 0xdeadbeefu);
+            PS::SIMDPOLY::PrintThreadResults(2, pr2.data());  // nothing accumulated since: no entry
+            std::ofstream o(argv[4], std::ios::binary);
+            put(o, rc1);
+            put(o, rc2);
+            put(o, n);
+            put(o, after);
+            o.write(reinterpret_cast<const char*>(pr.data()), (std::streamsize)n * 4);
+            o.write(reinterpret_cast<const char*>(cr.data()), (std::streamsize)n * 4);
+            o.write(reinterpret_cast<const char*>(pr2.data()), 16);
+            o.write(reinterpret_cast<const char*>(poly->vMPUs), (std::streamsize)poly->ctMPUs * sizeof(PsMPU));
             return 0;
         }
         const int rc = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *poly, NULL);  // the reference's default

@@ -236,6 +236,33 @@ def test_cpp_ps_simdpoly_polygonize(exe, tmp_path, oracle, name):
         np.testing.assert_array_equal(mpus["triangles"][i, :nt * 3].reshape(-1, 3), om.tris[t0:t0 + nt])
 
 
+@pytest.mark.gpu
+def test_cpp_ps_simdpoly_print_thread_results(exe, tmp_path):
+    """PS::SIMDPOLY::PrintThreadResults (PS_Polygonizer.h:393, .cpp:414-428) after two
+    Polygonize calls on C2: one worker (the calling thread's default context) whose counts,
+    divided by ctAttempts = 2, are the MPUs of one call and those with ctTriangles > 0; the
+    reference's lines on stdout; a second call finds nothing (the counters were cleared)."""
+    model, cs, _ = synth.make_config("C2")
+    src, out = tmp_path / "soa.bin", tmp_path / "threads.bin"
+    with open(src, "wb") as f:
+        f.write(model.prims.tobytes() + model.mats.tobytes() + model.ops.tobytes() + model.boxmats.tobytes())
+    r = subprocess.run([exe, "soa-threads", str(src), repr(float(cs)), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(out, "rb").read()
+    rc1, rc2, n, after = np.frombuffer(raw[:16], np.int32)
+    assert rc1 == rc2 == soa.RET_SUCCESS and n == 1 and after == 0
+    pr, cr = np.frombuffer(raw[16:16 + 8 * n], np.uint32).reshape(2, n)
+    pr2 = np.frombuffer(raw[16 + 8 * n:32 + 8 * n], np.uint32)
+    mpus = np.frombuffer(raw[32 + 8 * n:], soa.MPU_DTYPE)
+    assert len(mpus) == 6859
+    crossed = int((mpus["ctTriangles"] > 0).sum())
+    assert int(pr.sum()) == 6859 and int(cr.sum()) == crossed > 0
+    assert (pr2 == 0xdeadbeef).all()  # no entry: nothing written
+    lines = [l for l in r.stdout.splitlines() if l.startswith("Thread#")]
+    assert lines == [f"Thread#  1, Processed MPUs 6859, Crossed MPUs {crossed} "]
+
+
 # ---- compat mode: COMPACTBLOBTREE::convert and CParsipOptimized in C++ (parsip_gpu_gui.hpp)
 def cpp_compact(exe, root, tmp_path):
     tree, out = tmp_path / "tree.txt", tmp_path / "compact.bin"

@@ -88,6 +88,30 @@ def test_group_c3_eight_balanced_parts_equal_golden(group8):
     assert L is not None
 
 
+def test_print_thread_results_one_entry_per_part(oracle):
+    """PrintThreadResults over a 2-part group (two contexts = two workers) after two runs of
+    C2: entry k holds part k's MPUs and MPUs with triangles (summed, / ctAttempts), in the
+    order the parts first finished; the sums are the oracle's MPUs and surface MPUs."""
+    m, cs, _ = synth.make_config("C2")
+    om = oracle.polygonize(m, cs, threads=8)
+    g = gpu.Group([0, 0])
+    try:
+        g.set_model(m)
+        gpu.PrintThreadResults(1, echo=False)  # clear what earlier tests left
+        for _ in range(2):
+            info, parts = g.run(cs)
+        n = gpu.thread_result_count()
+        assert n == 2
+        pr, cr = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        assert gpu.PrintThreadResults(2, pr, cr) == 2
+        assert gpu.thread_result_count() == 0
+        assert list(pr) == [parts[k].info.ctMPUs for k in range(2)]
+        assert list(cr) == [parts[k].info.ctSurfaceMPUs for k in range(2)]
+        assert int(pr.sum()) == len(om.stats) and int(cr.sum()) == int((om.stats[:, 3] > 0).sum())
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("policy", [gpu.BALANCE_EVEN, gpu.BALANCE_EVERY_RUN])
 def test_group_c2_policies_match_oracle(group8, oracle, policy):
     model, cs, _ = synth.make_config("C2")

@@ -181,6 +181,45 @@ def test_fused_surface_golden(gpu_poly, name):
         gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
 
 
+@pytest.mark.parametrize("hook,fused", [(gpu.DEBUG_SURFACE_LATE_SCAN, 1), (gpu.DEBUG_LOOKBACK_TIMEOUT, 1),
+                                        (gpu.DEBUG_LOOKBACK_TIMEOUT, 0)])
+def test_protocol_error_reruns_two_kernels(gpu_poly, capfd, hook, fused):
+    """An in-kernel wait that gives up does not fail the call: k_surface's waves waiting for a
+    late offsets scan (hook 25: the scan blocks count themselves done ~40 us late, the waves
+    give up after a few spins), or a look-back that times out (hook 26, in k_surface's scan
+    blocks or k_vertex's) flag the run, and psgpu_finish re-runs it once as k_vertex +
+    k_finish: RET_SUCCESS and the committed C2 oracle digests.  The hooks apply to one run."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))["C2"]
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+
+    def digest():
+        gm, gs = gpu_poly.download(), gpu_poly.stats()
+        st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+        return mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris())
+    try:
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 1)
+        gpu_poly.jit_wait()
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, fused)
+        gpu_poly.run(cs)  # sizes the buffers; no hook
+        capfd.readouterr()
+        gpu_poly.set_option(gpu.OPT_DEBUG, hook)
+        info = gpu_poly.run(cs)  # raises PsgpuError on anything but RET_SUCCESS
+        err = capfd.readouterr().err
+        assert "re-running as k_vertex + k_finish" in err, err
+        assert ("k_surface" in err) == (fused == 1)
+        assert (info.ctVertices, info.ctTriangles) == (32541, 50034)
+        assert digest() == dig
+        gpu_poly.run(cs)  # the hook is spent: no error, no re-run
+        assert "protocol error" not in capfd.readouterr().err
+        assert digest() == dig
+    finally:
+        gpu_poly.set_option(gpu.OPT_DEBUG, 0)
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
+
+
 def test_engines_pipelined_c3_golden():
     """The bench's pipelining: 4 contexts take 12 C3 polygonizations in turn, queued without
     host synchronisation (bench.py's timed loop); every context's last mesh equals the

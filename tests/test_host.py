@@ -112,6 +112,24 @@ def test_no_device_fails_loudly():
         gpu.Polygonizer(0)
 
 
+def test_print_thread_results_host_contract(capfd):
+    """PrintThreadResults' host side: ctAttempts <= 0 is a parameter error (the reference
+    divides by it) and clears nothing; with no polygonization since the last call there is no
+    worker entry, nothing is written or printed."""
+    L = gpu.load()
+    assert L.psgpu_print_thread_results(0, None, None, 0, 1) == soa.RET_PARAM_ERROR
+    assert L.psgpu_print_thread_results(-3, None, None, 0, 1) == soa.RET_PARAM_ERROR
+    if gpu.device_count() > 0:
+        gpu.PrintThreadResults(1, echo=False)  # clear what earlier GPU tests of this process left
+    assert gpu.thread_result_count() == 0
+    p = np.full(4, 7, np.uint32)
+    assert gpu.PrintThreadResults(3, p, None) == 0
+    assert (p == 7).all()
+    assert "Thread#" not in capfd.readouterr().out
+    with pytest.raises(ValueError):
+        gpu.PrintThreadResults(1, np.zeros(4, np.int64))
+
+
 def test_bench_ranks_end_together_without_devices():
     """`bench.py --gpus 2` spawns its ranks; a rank without a HIP device exits with a
     message, and the parent ends the other ranks instead of leaving them in the rendezvous."""
@@ -165,6 +183,12 @@ def test_generated_kernels_resources():
         sgpr_ok = r["sgpr_spill"] <= (16 if name == "jit_surface" else 0)
         assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and sgpr_ok, (name, r)
         assert r["waves_per_simd"] >= want, (name, r["waves_per_simd"], r["limited_by"], r["vgpr"], r["sgpr"])
+    # k_surface reads the offsets its own scan blocks wrote with no acquire (an agent-scope
+    # acquire invalidates the XCD's L2 on gfx950): the 64-bit agent-scope loads must keep the
+    # sc1 bit that sends them past the non-coherent caches -- the look-back's, and the offsets
+    # reads of the vertex and triangle passes (surface_offs); k_vertex has the look-back's only
+    assert ks["jit_surface"]["load_x2_sc1"] >= 3, ks["jit_surface"]
+    assert ks["jit_vertex"]["load_x2_sc1"] >= 1, ks["jit_vertex"]
 
 
 _JIT_TREES = r"""
