@@ -176,8 +176,12 @@ typedef struct PsMeshInfo {
     uint64_t ctLaneEvals;       /* field evaluations performed (per point)          */
     uint32_t ctFieldMPUs;       /* S1 survivors whose 8^3 field cache was evaluated
                                  * (the rest were proven empty by field bounds)     */
-    uint32_t reserved;
+    uint32_t launchFlags;       /* how the run was launched: PSGPU_LAUNCH_*         */
 } PsMeshInfo;
+#define PSGPU_LAUNCH_TREE_SPLIT 1u  /* k_precheck / k_mpu walked the root's subtrees in two waves */
+#define PSGPU_LAUNCH_SURFACE    2u  /* k_vertex + k_finish ran as one launch (k_surface)         */
+#define PSGPU_LAUNCH_FRONT      4u  /* k_precheck + k_mpu ran as one launch (k_front)            */
+#define PSGPU_LAUNCH_RERUN      8u  /* finish re-ran the run (grid / capacity / protocol error)  */
 
 /* Device-resident compact mesh of the last polygonization (pointers into the
  * context's HBM buffers; valid until the next psgpu_polygonize on the context).
@@ -300,12 +304,15 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        staging past the piece flags is filled with the call's
                                        epoch before the export / the packing kernel's last
                                        block waits ~40 us before each piece;
-                                       bits 25 / 26 (test hooks, the next run only): k_surface's
-                                       scan blocks count themselves done ~40 us late and its
-                                       waves give up waiting after a few spins / every
-                                       offsets-scan look-back times out; either way finish
-                                       sees the protocol error and re-runs the polygonization
-                                       as k_vertex + k_finish (a second error: -6) */
+                                       bits 25 / 26 / 27 (test hooks, the next run only):
+                                       k_surface's scan blocks count themselves done ~40 us
+                                       late and its waves give up waiting after a few spins /
+                                       every offsets-scan look-back times out / k_front's S1
+                                       blocks publish ~40 us late and its S2 waves give up
+                                       after a few polls; either way finish sees the protocol
+                                       error and re-runs the polygonization as separate
+                                       launches (k_precheck, k_mpu, k_vertex, k_finish; a
+                                       second error: -6) */
 #define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU; once a
                                              run of the same range has finished, the grid is fitted
                                              to its vertices (+1/8) up to this (env PSGPU_GRID_FIT=0:
@@ -360,6 +367,11 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        run's vertices take the quad layouts in both (small rank
                                        shares), 1 always, 0 never.  Needs the small-launch kernels,
                                        compiled with PSGPU_OPT_TREE_SPLIT != 0.  Identical output */
+#define PSGPU_OPT_FRONT        22   /* k_precheck + k_mpu as one launch, S1 survivors handed to the
+                                       S2 blocks of the same launch as they are published (no grid
+                                       barrier): 0 (default) two launches, 1 always (with the
+                                       generated kernels), 2 for the tree-split small launches;
+                                       env PSGPU_FRONT; never with PSGPU_OPT_MPU_TICKS */
 #define PSGPU_OPT_MPU_TICKS    19   /* 1: runs record per-MPU ticks for MPUSTATS
                                        (psgpu_download_process_stats); 0 (default) off */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the

@@ -707,8 +707,9 @@ struct InterpEval {
 // records {start, end, item | hw id << 32} in the 100 MHz s_memrealtime clock, item = the
 // MPU a k_mpu wave polygonized (0xffffffff: none) or the wave's global index.
 __device__ __forceinline__ uint64_t stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
-__device__ __forceinline__ void stamp_end(const Params& p, int K, uint64_t t0, uint32_t item) {
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+__device__ __forceinline__ void stamp_end(const Params& p, int K, uint64_t t0, uint32_t item,
+                                          const uint32_t blk = blockIdx.x) {
+    const uint32_t w = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w >= p.stampCap) return;
     const uint64_t t1 = stamp_now();
     // HW_ID (CU, SIMD, SE; 32 bits) and XCC_ID (hwreg 20) as one word: hwid[15:0] | xcc << 16
@@ -829,7 +830,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_value(wav
 // (combine / bound_combine): the same values, half the walk per wave -- for launches whose
 // span is the heaviest brick's walk (small rank shares, a single engine).  Every wave of the
 // block reaches both barriers; the second wave of a brick stops after them.
-template <class EV, int SPLIT = 1>
+// k_front's tag of this run's queue entries: never 0 (the ready words start zeroed, and are
+// zeroed again whenever the counter sets restart from epoch 0)
+__device__ __forceinline__ uint32_t front_tag(const Params& p) { return p.ctr->epoch + 1u; }
+
+template <class EV, int SPLIT = 1, bool FRONT = false>
 __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const int wave = wave_index();
     const int lane = lane_id();
@@ -991,12 +996,17 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     const uint32_t shard = W / (p.pShardCap / 8u);
     if (lane == 1 && proven8 != 0u) atomicAdd(&p.ctr->shard[shard].b, (uint32_t)__popc(proven8));
     if (queue8 == 0u) return;
+    // k_front: the block's sub-queue (blockIdx mod 8, the XCD of round-robin placement: a speed
+    // choice only) at pq + q * fqCap, its count in shard q's p; otherwise the brick's shard
+    const uint32_t qsel = FRONT ? (blockIdx.x & 7u) : shard;
+    const uint32_t qbase = FRONT ? qsel * p.fqCap : shard * p.pShardCap;
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&p.ctr->shard[shard].p, (uint32_t)__popc(queue8));
+    if (lane == 0) base = atomicAdd(&p.ctr->shard[qsel].p, (uint32_t)__popc(queue8));
     base = lane_value(base, 0);
     if (pass) {
-        const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
-        p.pq[slotq] = mOf;
+        const uint32_t slotq = qbase + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
+        if (FRONT) __hip_atomic_store(&p.pq[slotq], mOf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+        else p.pq[slotq] = mOf;
         // the MPU's octants proven uniform by the same bounds: k_mpu evaluates only the others
         // (their inside bits are the proof's), bits 0-7 all outside, 8-15 all inside
         if (PSGPU_S2_OCT)
@@ -1016,14 +1026,29 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
             const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[1]), 8 * q));
             const float oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[2]), 8 * q));
             const CullMask g = cull_mask_from(cl, ox, oy, oz, ox + eg, oy + eg, oz + eg);
-            const uint32_t slotq = shard * p.pShardCap + base + (uint32_t)__popc(queue8 & ((1u << q) - 1u));
+            const uint32_t slotq = qbase + base + (uint32_t)__popc(queue8 & ((1u << q) - 1u));
             const uint32_t wq = lane_value(mOf, q) - p.mpuBegin;
             if (lane == 0) {
-                p.pqMask[2 * slotq] = g.lo;
-                p.pqMask[2 * slotq + 1] = g.hi;
+                if (FRONT) {  // read in this launch by S2 waves on other CUs: write-through (sc1)
+                    __hip_atomic_store(&p.pqMask[2 * slotq], g.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&p.pqMask[2 * slotq + 1], g.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    p.pqMask[2 * slotq] = g.lo;
+                    p.pqMask[2 * slotq + 1] = g.hi;
+                }
                 p.mpuMasks[2 * wq] = g.lo;
                 p.mpuMasks[2 * wq + 1] = g.hi;
             }
+        }
+    }
+    if constexpr (FRONT) {
+        // publish (MI355X_MICROARCH.md hand-off table, first row): the entries and masks were
+        // stored sc1; once they have left this wave (vmcnt(0)), each queued MPU's ready word
+        // takes the run's tag (sc1); S2 waves poll it with sc1 loads and then read the entry
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (pass) {
+            const uint32_t slotq = qbase + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
+            __hip_atomic_store(&p.fqReady[slotq], front_tag(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -1155,8 +1180,14 @@ __device__ __forceinline__ void s2_octants(const EV& ev, const float o[3], float
 // SPLIT 2 (tree split): two waves per MPU, each walking one subtree of the root over all
 // 8 x-slices (evaln_part), the values exchanged through LDS and combined by both waves
 // (combine), which then share the record passes as the W > 1 x-slice split does.
-template <class EV, int SPLIT = 1>
-__device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, uint32_t* item) {
+// FRONT (k_front, the S2 blocks of the launch whose first p.preBlocks blocks run S1): block blk
+// takes entries [MPB * (blk >> 3), MPB * (blk >> 3) + MPB) of sub-queue blk & 7 as their S1
+// waves publish them (their ready words carry the run's tag), instead of the d-th survivor
+// of the finished shard queues; an entry that is still untagged once every S1 block of its
+// sub-queue has published is past the sub-queue's end.
+template <class EV, int SPLIT = 1, bool FRONT = false>
+__device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, uint32_t* item,
+                                         const uint32_t blk = blockIdx.x) {
     *item = 0xffffffffu;
     constexpr int WPM = SPLIT > 1 ? SPLIT : kMpuWaves;  // waves per MPU
     constexpr int MPB = 4 / WPM;                         // MPUs per block
@@ -1169,33 +1200,85 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // the 64 shard queues: lane s holds shard s's count); the grid is sized by the host
     // from the last finished run, and a run with more survivors than that is re-run by finish()
     phase_stamp(p, 0);
-    const uint32_t d = blockIdx.x * (uint32_t)MPB + (uint32_t)slot;
+    uint32_t d = blk * (uint32_t)MPB + (uint32_t)slot;
     ModelPtr M = as_const(p.model);
     const CubeTablesDev* tab = p.tables;  // global: L1 / L2 resident (an LDS copy per block measured slower, r05)
-    // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
-    // the block
-    __shared__ uint32_t sIncl[kShards];
-    if (wave == 0) {
-        const uint32_t cnt = p.ctr->shard[lane].p;  // kShards == 64: one shard per lane
-        sIncl[lane] = wave_incl_scan(cnt);
+    bool live;
+    uint32_t slotq = 0;
+    if constexpr (FRONT) {
+        const uint32_t q = blk & 7u, e = (blk >> 3) * (uint32_t)MPB + (uint32_t)slot;
+        d = (e << 3) | q;  // spreads the MPU's vertex records over the shards
+        __shared__ uint32_t sFront[4];  // per MPU of the block: entry | live << 31
+        if (part == 0 && lane == 0) {
+            slotq = q * p.fqCap + e;
+            bool lv = false;
+            if (e < p.fqCap) {
+                const uint32_t tag = front_tag(p);
+                const uint32_t need = p.preBlocks > q ? (p.preBlocks - q + 7u) / 8u : 0u;  // S1 blocks of q
+                for (uint32_t spins = 0;; ++spins) {
+                    if (__hip_atomic_load(&p.fqReady[slotq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) {
+                        lv = true;
+                        break;
+                    }
+                    // every S1 block of q published (each after its waves' entries and tags left them)
+                    if ((spins & 7u) == 7u &&
+                        __hip_atomic_load(&p.ctr->shard[q].s1Done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) {
+                        lv = __hip_atomic_load(&p.fqReady[slotq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
+                        break;
+                    }
+                    // bounded (test hook PSGPU_OPT_DEBUG bit 27: a few spins against S1 blocks held
+                    // back ~40 us): a broken protocol is flagged, finish re-runs as separate launches
+                    if (spins > ((p.debug & (1u << 27)) ? 8u : (1u << 22))) {
+                        atomicOr(&p.ctr->error, 4u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            sFront[slot] = slotq | (lv ? 0x80000000u : 0u);
+        }
+        __syncthreads();  // the MPU's other wave reads the entry after the barrier its poller joined
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < MPB; ++k) any |= (sFront[k] >> 31) != 0u;
+        if (!any) return;  // no entry for this block (block-uniform)
+        slotq = sFront[slot] & 0x7fffffffu;
+        live = (sFront[slot] >> 31) != 0u;
+    } else {
+        // prologue: wave 0 reads the 64 shard counts (one 128-B line each) and scans them for
+        // the block
+        __shared__ uint32_t sIncl[kShards];
+        if (wave == 0) {
+            const uint32_t cnt = p.ctr->shard[lane].p;  // kShards == 64: one shard per lane
+            sIncl[lane] = wave_incl_scan(cnt);
+        }
+        __syncthreads();
+        // MPU d = block * (4 / W) + slot is the d-th queued survivor in shard order (dense over
+        // the 64 shard queues); the grid is sized by the host from the last finished run, and
+        // a run with more survivors than that is re-run by finish()
+        const uint32_t incl = sIncl[lane];
+        const uint32_t pcount = sIncl[kShards - 1];
+        if (blk * (uint32_t)MPB >= pcount) return;  // whole block past the last survivor
+        live = d < pcount;
+        if (live) {
+            const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
+            const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
+            slotq = uniform(pshard * p.pShardCap + pidx);
+        }
     }
-    __syncthreads();
-    // MPU d = block * (4 / W) + slot is the d-th queued survivor in shard order (dense over
-    // the 64 shard queues); the grid is sized by the host from the last finished run, and
-    // a run with more survivors than that is re-run by finish()
-    const uint32_t incl = sIncl[lane];
-    const uint32_t pcount = sIncl[kShards - 1];
-    if (blockIdx.x * (uint32_t)MPB >= pcount) return;  // whole block past the last survivor
-    const bool live = d < pcount;
     uint32_t m = 0, w = 0;
     float o[3] = {0.0f, 0.0f, 0.0f};
     CullMask cm{0ull, 0ull};
     uint32_t oct = 0;  // k_precheck's octant proofs (PSGPU_S2_OCT)
     (void)oct;
     if (live) {
-        const uint32_t pshard = (uint32_t)__popcll(ballot(incl <= d));  // first shard whose prefix passes d
-        const uint32_t pidx = d - (pshard ? sIncl[pshard - 1] : 0u);
-        const uint32_t slotq = uniform(pshard * p.pShardCap + pidx);
+        if (FRONT) {  // published in this launch: sc1 loads (the stores were sc1)
+            m = uniform(__hip_atomic_load(&p.pq[slotq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (p.cull) {
+                cm.lo = uniform64(__hip_atomic_load(&p.pqMask[2 * slotq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                cm.hi = uniform64(__hip_atomic_load(&p.pqMask[2 * slotq + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+        } else {
         m = uniform(p.pq[slotq]);
         if (p.cull) {  // the MPU box's culling mask, made by k_precheck: in SGPRs, so every
                        // per-primitive culling test of the walk is a scalar branch
@@ -1206,6 +1289,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
             cm.lo = p.pqMask[2 * slotq];
             cm.hi = p.pqMask[2 * slotq + 1];
 #endif
+        }
         }
         if (PSGPU_S2_OCT) oct = uniform((uint32_t)p.pqOct[slotq]);
         *item = m;
@@ -1876,7 +1960,10 @@ __device__ __forceinline__ void finish_body(const Params& p, float* lds) {
         __threadfence_system();
         // the next run's counters and offsets-scan words (no kernel of this run touches them)
         uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
-        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
+        const uint32_t nextEpoch = p.ctr->epoch + 1u;
+        constexpr uint32_t kEpochWord = __builtin_offsetof(DevCounters, epoch) / 4;
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x)
+            nx[i] = i == 0 ? 0x7fffffffu : (i == kEpochWord ? nextEpoch : 0u);
         for (uint32_t i = threadIdx.x; i < kScanMaxBlocks; i += blockDim.x) p.scanStatusNext[i] = 0ull;
         if (threadIdx.x < 64) {  // the run's totals for the count exchange between parts (RCCL)
             const ShardCtr& sc = p.ctr->shard[threadIdx.x];
@@ -2113,6 +2200,46 @@ if constexpr (VPW == 16) {
     phase_stamp_after(p, 6, 2048u, 0.0f);
 }
 
+// k_front (PSGPU_OPT_FRONT): k_precheck and k_mpu as one launch for small launches, with a
+// dataflow hand-over instead of the kernel boundary (no grid barrier: r05's barrier version,
+// k_front v1-v3 in profiles/r05_front_ab.txt, was slower than the boundary).  Blocks
+// [0, preBlocks) run S1 exactly as k_precheck and publish each queued MPU (sc1 entry and
+// culling mask, then the entry's ready word with the run's tag) into sub-queue blockIdx & 7;
+// when all of a block's waves have published, its last wave counts the block done for its
+// sub-queue.  The blocks after them run S2-S3 exactly as k_mpu on entries as they are
+// published.  Every S1 block is dispatched before any S2 block (in-order dispatch), so a
+// waiting S2 block never holds back the S1 block it waits for; every wait is bounded and a
+// timeout fails the run as a protocol error (finish re-runs it as separate launches).
+template <class EV, int SPLIT>
+__device__ __forceinline__ void front_body(const Params& p, unsigned char* smem) {
+    const uint64_t t0 = (p.stamps || p.spans) ? stamp_now() : 0ull;
+    if (blockIdx.x < p.preBlocks) {  // block-uniform
+        __shared__ uint32_t sArrive;
+        if (threadIdx.x == 0) {
+            sArrive = 0u;
+            if (p.debug & (1u << 27)) {  // test hook: the S1 blocks publish ~40 us late
+                const uint64_t h0 = stamp_now();
+                while (stamp_now() - h0 < 4000u) __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        __syncthreads();
+        precheck_body<EV, SPLIT, true>(p, reinterpret_cast<float*>(smem));
+        if (p.stamps) stamp_end(p, 0, t0, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        if (p.spans) span_end(p, 0, t0);
+        // the block's arrival: each wave after its own stores left it; the last one signals
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane_id() == 0 && atomicAdd(&sArrive, 1u) == (blockDim.x >> 6) - 1u)
+            __hip_atomic_fetch_add(&p.ctr->shard[blockIdx.x & 7u].s1Done, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        const uint32_t blk = blockIdx.x - p.preBlocks;
+        uint32_t item = 0xffffffffu;
+        mpu_body<EV, SPLIT, true>(p, smem, &item, blk);
+        if (p.stamps) stamp_end(p, 1, t0, item, blk);
+        if (p.spans) span_end(p, 1, t0);
+    }
+}
+
 // k_surface's wait for the offsets scan (every scan block released its offsets), bounded: a
 // broken protocol flags the run (error bit 1) instead of hanging the device.
 // The flag reaches the host through words block 0 never overwrites (surfaceErr, raised with
@@ -2188,7 +2315,10 @@ __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
             if (i != kSurfWord) dst[i] = i == kErrWord ? err : src[i];
         __threadfence_system();
         uint32_t* nx = reinterpret_cast<uint32_t*>(p.ctrNext);
-        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x) nx[i] = i == 0 ? 0x7fffffffu : 0u;
+        const uint32_t nextEpoch = p.ctr->epoch + 1u;
+        constexpr uint32_t kEpochWord = __builtin_offsetof(DevCounters, epoch) / 4;
+        for (uint32_t i = threadIdx.x; i < sizeof(DevCounters) / 4; i += blockDim.x)
+            nx[i] = i == 0 ? 0x7fffffffu : (i == kEpochWord ? nextEpoch : 0u);
         for (uint32_t i = threadIdx.x; i < kScanMaxBlocks; i += blockDim.x) p.scanStatusNext[i] = 0ull;
         if (threadIdx.x < 64) {
             const ShardCtr& sc = p.ctr->shard[threadIdx.x];

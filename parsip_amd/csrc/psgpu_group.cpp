@@ -333,6 +333,7 @@ int psgpu_group_finish(psgpu_group* g, PsMeshInfo* totalOut, PsGroupPart* partsO
             T.ctSurfaceMPUs += I.ctSurfaceMPUs;
             T.ctLaneEvals += I.ctLaneEvals;
             T.ctFieldMPUs += I.ctFieldMPUs;
+            T.launchFlags |= I.launchFlags;  // any part's
             if (I.firstOverflowMPU >= 0 && T.firstOverflowMPU < 0) T.firstOverflowMPU = I.firstOverflowMPU;
         }
         if (v > 0xffffffffull || t > 0xffffffffull) return PSGPU_RET_NOT_ENOUGH_MEM;

@@ -445,11 +445,26 @@ bool s2_oct_enabled() {
     return on;
 }
 
+// k_front sub-queue capacity for a k_precheck grid of `blocks` blocks of `mpb` bricks: every
+// 8th block's bricks x 8 MPUs; front_cap(bricks) bounds it for both grids (2 and 4 bricks per block)
+uint32_t front_sub_cap(uint32_t blocks, uint32_t mpb) { return 8u * mpb * ((blocks + 7u) / 8u); }
+uint32_t front_cap(size_t bricks) {
+    const uint32_t b = (uint32_t)bricks;
+    return std::max(front_sub_cap((b + 1u) / 2u, 2u), front_sub_cap((b + 3u) / 4u, 4u));
+}
+
 int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
     const size_t n = std::max<uint32_t>(mpuCount, 1);
     c->pShardCap = 8u * (uint32_t)((brick_count(c) + kShards - 1) / kShards);
-    PSGPU_CHECK(grow(c->pq, c->capList, (size_t)c->pShardCap * kShards));
-    PSGPU_CHECK(grow(c->pqMask, c->capPqMask, (size_t)c->pShardCap * kShards * 2));
+    // k_front's 8 sub-queues: a block's bricks x 8 MPUs for every 8th k_precheck block
+    const size_t fq = 8 * front_cap(brick_count(c));
+    const size_t nq = std::max<size_t>((size_t)c->pShardCap * kShards, fq);
+    PSGPU_CHECK(grow(c->pq, c->capList, nq));
+    PSGPU_CHECK(grow(c->pqMask, c->capPqMask, nq * 2));
+    if (fq > c->capFq) {  // ready words start at 0: no run's tag
+        PSGPU_CHECK(grow(c->fqReady, c->capFq, fq));
+        PSGPU_CHECK(hipMemset(c->fqReady, 0, c->capFq * sizeof(uint32_t)));
+    }
     if (s2_oct_enabled()) PSGPU_CHECK(grow(c->pqOct, c->capPqOct, (size_t)c->pShardCap * kShards));
     PSGPU_CHECK(grow(c->counts, c->capCounts, n));
     PSGPU_CHECK(grow(c->passed, c->capPassed, n));
@@ -473,6 +488,17 @@ int ensure_buffers(psgpu_ctx* c, uint32_t mpuCount) {
 bool use_split(const psgpu_ctx* c) {
     if (!c->jit || !c->jit->precheckS || !c->splittable) return false;
     return c->treeSplit == 1 || (c->treeSplit == 2 && c->haveQueued && c->lastQueued <= c->splitMaxQueued);
+}
+
+// k_precheck + k_mpu as one launch (k_front) for the next run: 1 forces it, 2 for the split
+// kernels' small launches (use_split); never with per-MPU ticks (MPUSTATS: S1 and S2 would
+// write an MPU's tick words from two XCDs in one launch) or while finish re-runs a run whose
+// in-kernel wait gave up (surfaceOff)
+bool use_front(const psgpu_ctx* c) {
+    if (!c->jit || c->front == 0 || c->surfaceOff || c->mpuTicksOpt) return false;
+    const bool split = use_split(c);
+    if (!(split ? c->jit->frontS : c->jit->front)) return false;
+    return c->front == 1 || split;
 }
 
 Params make_params(psgpu_ctx* c) {
@@ -506,7 +532,17 @@ Params make_params(psgpu_ctx* c) {
     const uint32_t margin = c->lastQueued / c->mpuMarginDiv + (c->mpuMarginDiv > 4 ? 64u : 256u);
     const uint32_t want = c->haveQueued ? (c->lastQueued + margin + mpb - 1) / mpb : maxBlocks;
     p.mpuBlocks = std::max(1u, std::min(maxBlocks, want));
-    if (c->debug & (1 << 20)) p.mpuBlocks = 1;  // test hook: a k_mpu grid that falls short (finish re-runs)
+    p.fqReady = c->fqReady;
+    p.fqCap = front_sub_cap(p.preBlocks, mpb);
+    if (use_front(c)) {
+        // k_front's S2 blocks: 8 per row, a row takes mpb entries of each sub-queue; rows for the
+        // last run's largest sub-queue + 1/4 (or every entry of a sub-queue without a last run)
+        const uint32_t sub = !c->haveQueued ? p.fqCap
+                             : (c->lastSubMax ? c->lastSubMax : (c->lastQueued + 7u) / 8u) + c->lastQueued / 32u + 32u;
+        const uint32_t rows = (std::min(sub, p.fqCap) + mpb - 1u) / mpb;
+        p.mpuBlocks = 8u * std::max(1u, rows);
+    }
+    if (c->debug & (1 << 20)) p.mpuBlocks = use_front(c) ? 8u : 1u;  // test hook: a k_mpu grid that falls short (finish re-runs)
     p.scanChunks = (c->mpuCount + kScanItems * kScanMaxBlocks - 1) / (kScanItems * kScanMaxBlocks);
     if (p.scanChunks == 0) p.scanChunks = 1;
     p.scanBlocks = (c->mpuCount + kScanItems * p.scanChunks - 1) / (kScanItems * p.scanChunks);
@@ -595,6 +631,14 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     JitKernels* J = c->jit.get();
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[0], s));
     const bool split = use_split(c);
+    if (use_front(c)) {  // S1 blocks, then S2 blocks taking the survivors as they are published
+        PSGPU_CHECK(launch_jit(split ? J->frontS : J->front, p.preBlocks + p.mpuBlocks, 256,
+                               mpu_lds_bytes(0) / (split ? 2 : 1), s, p));
+        if (timed) {
+            PSGPU_CHECK(hipEventRecord(c->ev[1], s));
+            PSGPU_CHECK(hipEventRecord(c->ev[2], s));
+        }
+    } else {
     if (J) PSGPU_CHECK(launch_jit(split ? J->precheckS : J->precheck, p.preBlocks, 256, 0, s, p));
     else PSGPU_CHECK(launch_precheck(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[1], s));
@@ -602,6 +646,7 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
     if (J) PSGPU_CHECK(launch_jit(split ? J->mpuS : J->mpu, p.mpuBlocks, 256, mpu_lds_bytes(0) / (split ? 2 : 1), s, p));
     else PSGPU_CHECK(launch_mpu(p, s));
     if (timed) PSGPU_CHECK(hipEventRecord(c->ev[2], s));
+    }
     // k_vertex's first scanBlocks blocks also compute the mesh offsets (all co-resident)
     const int vpwV = J ? vertex_vpw(c) : 16;
     uint32_t gridV = std::max(persistV, p.scanBlocks);
@@ -659,7 +704,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     const Params p = make_params(c);
     c->runTicks = p.mpuTicks != nullptr;
-    c->debug &= ~((1 << 20) | (1 << 25) | (1 << 26));  // the short-grid / protocol test hooks apply to one run
+    c->debug &= ~((1 << 20) | (1 << 25) | (1 << 26) | (1 << 27));  // the short-grid / protocol test hooks apply to one run
     if (p.spans) c->spanNext++;
     c->runMpuBlocks = p.mpuBlocks;
     c->runMpb = use_split(c) ? 2u : (uint32_t)kMpusPerBlock;
@@ -667,6 +712,8 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     c->parity ^= 1u;  // k_finish of this run resets the other set for the next run
     const bool timed = c->timing != 0;
     c->runSurface = use_surface(c);
+    c->runFront = use_front(c);
+    c->runSplit = use_split(c);
     if (c->stamps)  // waves that do not run leave no stale records
         PSGPU_CHECK(hipMemsetAsync(c->stamps, 0, (size_t)kNumStampKernels * c->stampCap * 24 + (size_t)c->stampCap * 64, s));
     if (!c->useGraph || timed || s == nullptr) {
@@ -676,7 +723,8 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
     }
     psgpu_ctx::GraphSlot& g = c->graphs[slot];
     const uint32_t shape[6] = {(uint32_t)c->vertexBlocksPerCU, (uint32_t)c->finishBlocksPerCU, (uint32_t)c->numCUs,
-                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c), (use_split(c) ? 1u : 0u) | (use_surface(c) ? 2u : 0u)};
+                               (uint32_t)finish_vpw(c), (uint32_t)vertex_vpw(c),
+                               (use_split(c) ? 1u : 0u) | (use_surface(c) ? 2u : 0u) | (use_front(c) ? 4u : 0u)};
     if (!(g.exec && g.jit == c->jit.get() && memcmp(&g.key, &p, sizeof(Params)) == 0 &&
           memcmp(g.shape, shape, sizeof(shape)) == 0)) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -823,6 +871,7 @@ void reset_run_state(psgpu_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipMemcpy(c->ctr, init, sizeof(init), hipMemcpyHostToDevice);
     (void)hipMemset(c->scanStatus, 0, 2 * kScanMaxBlocks * sizeof(uint64_t));
+    if (c->fqReady) (void)hipMemset(c->fqReady, 0, c->capFq * sizeof(uint32_t));  // the epochs restart at 0
     (void)hipDeviceSynchronize();
     c->parity = 0;
     drop_graphs(c);
@@ -1049,6 +1098,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (const char* e = getenv("PSGPU_VERTEX_WIDE")) c->vertexWide = std::min(2, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_MPU_MARGIN")) c->mpuMarginDiv = std::max(1, atoi(e));
     if (const char* e = getenv("PSGPU_FUSED_SURFACE")) c->fusedSurface = std::min(2, std::max(0, atoi(e)));
+    if (const char* e = getenv("PSGPU_FRONT")) c->front = std::min(2, std::max(0, atoi(e)));
     *out = c;
     return PSGPU_RET_SUCCESS;
 }
@@ -1069,7 +1119,7 @@ void psgpu_destroy(psgpu_ctx* c) {
     c->tier2Fut = JitFuture();
     c->jit.reset();
     c->jit1.reset();
-    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->pqOct, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
+    void* bufs[] = {c->dModel, c->dTables, c->pq, c->pqMask, c->pqOct, c->fqReady, c->scanStatus, c->counts, c->passed, c->mpuMasks, c->offs, c->vk, c->vp, c->tq,
                     c->pos, c->nrm, c->col, c->tris, c->ctr, c->totals, c->stamps, c->spans, c->mpuTicks};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1126,6 +1176,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
     }
     else if (option == PSGPU_OPT_SPLIT_MAX_QUEUED && value >= 0 && value <= 0xffffffffll) c->splitMaxQueued = (uint32_t)value;
     else if (option == PSGPU_OPT_FUSED_SURFACE && value >= 0 && value <= 2) c->fusedSurface = (int)value;
+    else if (option == PSGPU_OPT_FRONT && value >= 0 && value <= 2) c->front = (int)value;
     else if (option == PSGPU_OPT_TIER_RUNS && value >= 1 && value <= (1 << 30)) c->tierRuns = (int)value;
     else if (option == PSGPU_OPT_JIT) {
         if (value < 0 || value > 3) return PSGPU_RET_PARAM_ERROR;
@@ -1257,6 +1308,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         PSGPU_CHECK(hipStreamSynchronize(c->runStream));
         set_pending(c, false);
         // grow and re-run if the work queues or the compact outputs did not fit
+        bool reran = false;
         for (int attempt = 0; attempt < 4; ++attempt) {
             const DevCounters& h = *c->hostCtr;
             uint32_t V = 0, T = 0, mv = 0, mt = 0, Q = 0;
@@ -1267,7 +1319,15 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
                 mv = std::max(mv, h.shard[k].v);
                 mt = std::max(mt, h.shard[k].t);
             }
-            const bool gridShort = c->mpuCount > 0 && Q > c->runMpb * c->runMpuBlocks;
+            bool gridShort = c->mpuCount > 0 && Q > c->runMpb * c->runMpuBlocks;
+            if (c->runFront) {  // k_front: each sub-queue against its own rows of S2 blocks
+                uint32_t sub = 0;
+                for (int k = 0; k < 8; ++k) sub = std::max(sub, h.shard[k].p);
+                gridShort = c->mpuCount > 0 && sub > c->runMpb * (c->runMpuBlocks / 8u);
+                c->lastSubMax = sub;
+            } else {
+                c->lastSubMax = 0;
+            }
             c->lastQueued = Q;
             c->lastV = V;
             c->haveQueued = c->mpuCount > 0;
@@ -1286,6 +1346,7 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             rc = enqueue(c, c->runStream);
             if (rc != PSGPU_RET_SUCCESS) return rc;
             PSGPU_CHECK(hipStreamSynchronize(c->runStream));
+            reran = true;
         }
         if (c->timing && c->mpuCount > 0) {
             for (int k = 0; k < kNumKernels; ++k) {
@@ -1298,13 +1359,15 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
             // an in-kernel wait gave up (an offsets-scan look-back, or k_surface's wait for the
             // scan): the run's offsets are not trusted.  Re-run it once as k_vertex + k_finish,
             // the chain whose kernel boundaries order the scan; a second error fails the call.
-            fprintf(stderr, "psgpu: device protocol error 0x%x (%s): re-running as k_vertex + k_finish\n",
-                    h.error | h.surfaceErr, c->runSurface ? "k_surface" : "k_vertex");
+            fprintf(stderr, "psgpu: device protocol error 0x%x (%s): re-running as separate launches\n",
+                    h.error | h.surfaceErr, c->runFront ? (c->runSurface ? "k_front, k_surface" : "k_front")
+                                                        : (c->runSurface ? "k_surface" : "k_vertex"));
             c->surfaceOff = true;
             rc = enqueue(c, c->runStream);
             c->surfaceOff = false;
             if (rc != PSGPU_RET_SUCCESS) return rc;
             PSGPU_CHECK(hipStreamSynchronize(c->runStream));
+            reran = true;
             if (h.error | h.surfaceErr) {
                 fprintf(stderr, "psgpu: device protocol error 0x%x\n", h.error | h.surfaceErr);
                 return PSGPU_RET_DEVICE_ERROR;
@@ -1332,6 +1395,9 @@ int psgpu_finish(psgpu_ctx* c, PsMeshInfo* info) {
         I.firstOverflowMPU = (c->mpuCount && h.firstOverflow != 0x7fffffff) ? h.firstOverflow : -1;
         I.ctFieldMPUs = c->mpuCount ? Q : 0;
         I.ctLaneEvals = 8ull * c->mpuCount + 512ull * I.ctFieldMPUs + 8ull * I.ctVertices;
+        I.launchFlags = c->mpuCount == 0 ? 0u
+                        : (c->runSplit ? PSGPU_LAUNCH_TREE_SPLIT : 0u) | (c->runSurface ? PSGPU_LAUNCH_SURFACE : 0u) |
+                              (c->runFront ? PSGPU_LAUNCH_FRONT : 0u) | (reran ? PSGPU_LAUNCH_RERUN : 0u);
         c->haveResult = true;
         if (c->countThreads) thread_results_add(c->serial, I.ctMPUs, I.ctSurfaceMPUs);
     }

@@ -73,7 +73,13 @@ struct psgpu_ctx {
     bool splittable = false;  // the model's walk splits at the root (jit_splittable)
     int fusedSurface = 2;     // PSGPU_OPT_FUSED_SURFACE: k_vertex + k_finish in one launch (use_surface)
     bool runSurface = false;  // the last enqueued run took k_surface
-    bool surfaceOff = false;  // while finish re-runs a run whose in-kernel wait gave up: the two kernels
+    int front = 0;            // PSGPU_OPT_FRONT: k_precheck + k_mpu in one launch (use_front)
+    bool runFront = false;    // the last enqueued run took k_front
+    bool runSplit = false;    // ... and the tree-split kernels
+    uint32_t lastSubMax = 0;  // the largest k_front sub-queue of the last finished run (0: none)
+    uint32_t* fqReady = nullptr;  // k_front: per queue entry, the tag of the run that published it
+    size_t capFq = 0;
+    bool surfaceOff = false;  // while finish re-runs a run whose in-kernel wait gave up: the separate kernels
     uint32_t splitMaxQueued = 1024;  // PSGPU_OPT_SPLIT_MAX_QUEUED: tree split 2 applies up to this many S2 MPUs
                                      // (psgpu_create: 4 per CU; C3's 1/8 shares queue ~800, 1/4 ~1,600)
     uint32_t runMpb = 0;      // k_mpu MPUs per block of the last enqueued run

@@ -169,12 +169,13 @@ constexpr int kShards = 64;
 constexpr uint32_t kScanItems = 2048;   // offsets scan: counts per 256-thread block per chunk
 constexpr uint32_t kScanMaxBlocks = 256;
 struct ShardCtr {           // one 128-B line per shard: atomics on one line serialise
-    uint32_t p;             // S1 survivors appended
+    uint32_t p;             // S1 survivors appended (k_front: shards 0-7 are its 8 sub-queues)
     uint32_t v;             // vertex records appended
     uint32_t t;             // triangle records appended
     uint32_t s;             // surface MPUs (>= 1 triangle)
     uint32_t b;             // S1 survivors proven empty by field bounds (not queued)
-    uint32_t pad[27];
+    uint32_t s1Done;        // k_front, shards 0-7: S1 blocks of sub-queue k that published all entries
+    uint32_t pad[26];
 };
 struct DevCounters {
     int32_t firstOverflow;   // min global MPU id with > 512 V or T (INT32_MAX: none)
@@ -184,7 +185,9 @@ struct DevCounters {
     uint32_t surfaceErr;     // host copy only: 2 once a k_surface wave's scan wait timed out (plain
                              // stores of one value, so no read-modify-write over PCIe); zeroed by
                              // k_precheck, never copied from the device counters by k_surface
-    uint32_t pad[28];
+    uint32_t epoch;          // run sequence number: the previous run's last kernel sets it to its own
+                             // + 1 when it resets this set; k_front tags its queue entries with it + 1
+    uint32_t pad[27];
     ShardCtr shard[kShards];
 };
 
@@ -221,6 +224,8 @@ struct Params {
     uint64_t* pqMask;       // per queue entry: the MPU box's culling mask (2 words, by k_precheck)
     uint16_t* pqOct;        // per queue entry: octants proven all outside (bits 0-7) / inside (8-15)
     uint32_t pShardCap;     // 8 * ceil(precheck waves / kShards): cannot overflow
+    uint32_t* fqReady;      // k_front: per queue entry, the run's tag once the entry is published
+    uint32_t fqCap;         // k_front: entries per sub-queue (8 sub-queues at pq + k * fqCap)
     uint32_t mpuBlocks;     // k_mpu grid (4 waves per block, kMpusPerBlock queued survivors per block)
     uint64_t* counts;       // mpuCount: V | T << 32 per MPU of the range (0 if S1 failed)
     uint8_t* passed;        // mpuCount: 1 if the MPU passed S1 (PsMpuStats::passedPrecheck)

@@ -37,7 +37,7 @@ class PsMeshInfo(ctypes.Structure):
                 ("ctSurfaceMPUs", ctypes.c_uint32), ("ctVertices", ctypes.c_uint32),
                 ("ctTriangles", ctypes.c_uint32), ("firstOverflowMPU", ctypes.c_int32),
                 ("ctLaneEvals", ctypes.c_uint64), ("ctFieldMPUs", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("launchFlags", ctypes.c_uint32)]
 
 
 class PsGroupPart(ctypes.Structure):
@@ -86,8 +86,11 @@ OPT_SPLIT_MAX_QUEUED = 17
 OPT_TIER_RUNS = 18
 OPT_MPU_TICKS = 19
 OPT_FUSED_SURFACE = 21
+OPT_FRONT = 22
+LAUNCH_TREE_SPLIT, LAUNCH_SURFACE, LAUNCH_FRONT, LAUNCH_RERUN = 1, 2, 4, 8  # PsMeshInfo.launchFlags
 DEBUG_SURFACE_LATE_SCAN = 1 << 25  # test hooks of the in-kernel waits (OPT_DEBUG bits, one run each)
 DEBUG_LOOKBACK_TIMEOUT = 1 << 26
+DEBUG_FRONT_LATE_S1 = 1 << 27
 DEBUG_EXPORT_POISON = 1 << 23  # test hooks of the blocking export (OPT_DEBUG bits)
 DEBUG_EXPORT_STRAGGLER = 1 << 24
 JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values

@@ -1,7 +1,7 @@
 """Seeded fuzz parity: random trees over every primitive and operator type (warps included),
 random matrices, cell sizes off the round values, ragged MPU ranges (a rank's share starts and
 ends anywhere in the lattice), culling on and off, the interpreter and the generated kernels,
-every k_vertex / k_finish layout, the tree split and the fused k_surface -- the HIP path through the C-ABI against
+every k_vertex / k_finish layout, the tree split, the fused k_surface and k_front -- the HIP path through the C-ABI against
 the CPU oracle, bit-exact (tests/parity_util.py)."""
 import numpy as np
 import pytest
@@ -38,8 +38,10 @@ def test_fuzz_ranges_and_trees(gpu_poly, oracle, seed):
         gpu_poly.set_option(gpu.OPT_JIT, jit)
         gpu_poly.set_option(gpu.OPT_VERTEX_WIDE, vwide)
         gpu_poly.set_option(gpu.OPT_FINISH_QUAD, fquad)
-        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, split if jit else 0)
+        front = (seed // 2) % 3  # k_front (with the small-launch kernels: split 0 compiles them as 2)
+        gpu_poly.set_option(gpu.OPT_TREE_SPLIT, (split if split or not front else 2) if jit else 0)
         gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, seed % 3)  # k_surface when the split compiled it
+        gpu_poly.set_option(gpu.OPT_FRONT, front)
         gpu_poly.set_model(model)
         assert gpu_poly.jit_active == bool(jit)
         gpu_poly.run(cs, begin, end)
@@ -52,5 +54,6 @@ def test_fuzz_ranges_and_trees(gpu_poly, oracle, seed):
         gpu_poly.set_option(gpu.OPT_FINISH_QUAD, 2)
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
         gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
+        gpu_poly.set_option(gpu.OPT_FRONT, 0)
     om = oracle.polygonize(model, cs, begin, end, threads=8)
     assert_mesh_matches(gm, gs, om)
