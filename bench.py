@@ -412,15 +412,17 @@ class Engine:
         the per-wave timeline (OPT_STAMPS)."""
         if self.p is not None:
             info = self.p.finish()
-            return [(gpu.kernel_spans(self.p.stamps()), info.ctFieldMPUs)]
+            return [(gpu.kernel_spans(self.p.stamps(), bool(info.launchFlags & gpu.LAUNCH_FRONT)), info.ctFieldMPUs)]
         _, parts = self.obj.finish()
-        return [(gpu.kernel_spans(self.obj.stamps(i)), parts[i].info.ctFieldMPUs) for i in range(self.parts)]
+        return [(gpu.kernel_spans(self.obj.stamps(i), bool(parts[i].info.launchFlags & gpu.LAUNCH_FRONT)),
+                 parts[i].info.ctFieldMPUs) for i in range(self.parts)]
 
-    def spans(self):
-        """(launches, kernels) device-clock spans in ms recorded since OPT_SPANS, every part."""
+    def spans(self, raw=False):
+        """(launches, kernels) device-clock spans in ms recorded since OPT_SPANS, every part
+        (raw: (launches, kernels, {first wave start, last wave end}) in 100 MHz ticks)."""
         if self.p is not None:
-            return self.p.spans()
-        return np.concatenate([self.obj.spans(i) for i in range(self.parts)])
+            return self.p.spans(raw)
+        return np.concatenate([self.obj.spans(i, raw) for i in range(self.parts)])
 
     def close(self):
         if self.comm:
@@ -676,11 +678,18 @@ def main():
         engines[k % neng].polygonize()
     for e in engines:
         e.finish()
-    sp = np.concatenate([e.spans() for e in engines])
+    spr = np.concatenate([e.spans(raw=True) for e in engines])  # (launches, kernels, {start, end})
+    sp = (spr[:, :, 1] - spr[:, :, 0]) * 1e-5
     for e in engines:
         e.set_option(gpu.OPT_SPANS, 0)
     launches = len(sp)
     kt = {k: float(sp[:, i].mean()) for i, k in enumerate(gpu.STAMP_KERNELS)}
+    # k_front (PSGPU_OPT_FRONT): k_precheck's and k_mpu's waves are the S1 and S2 blocks of ONE
+    # launch; its span is theirs together
+    front = bool(mine.launchFlags & gpu.LAUNCH_FRONT)
+    if front:
+        kt["k_front"] = float(((np.maximum(spr[:, 0, 1], spr[:, 1, 1]) - np.minimum(spr[:, 0, 0], spr[:, 1, 0]))
+                               * 1e-5).mean())
     fmpus = sum(e.local_info().ctFieldMPUs for e in engines) / neng * launches / nparts
     # pass 2: hipEvent brackets around each kernel (they add the dispatch gap before each
     # launch), in bursts alternating between the engines; the sample is the run of the engine
@@ -702,6 +711,9 @@ def main():
     for e in engines:
         e.set_option(gpu.OPT_KERNEL_TIMING, 0)
     ev_ms = {k: v / ev_n for k, v in kt_sum.items()}
+    if front:  # the hipEvent pair before / after the one launch ("k_precheck"; "k_mpu" brackets nothing)
+        ev_ms["k_front"] = ev_ms.pop("k_precheck", 0.0)
+        ev_ms.pop("k_mpu", None)
     for e in engines:
         e.set_option(gpu.OPT_STAMPS, 1 << 17)
     # the same launches with the device to themselves (engine 0 alone): the per-kernel
@@ -718,22 +730,34 @@ def main():
         e.set_option(gpu.OPT_STAMPS, 0)
     solo = {k: v / solo_n for k, v in solo_sum.items()}
     single = mine
-    # the dominant kernel: the longest with the device to itself (the replay spans of
-    # concurrent engines stretch whichever kernel overlaps the other engine's work)
-    dom = max(solo, key=solo.get) if solo else max(kt, key=kt.get)
+    # the dominant kernel: the longest launch with the device to itself (the replay spans of
+    # concurrent engines stretch whichever kernel overlaps the other engine's work); with
+    # k_front, its S1 / S2 wave spans are reported but the launch is k_front
+    launch_names = [k for k in solo if not (front and k in ("k_precheck", "k_mpu"))]
+    dom = max(launch_names, key=solo.get) if launch_names else max(kt, key=kt.get)
     # lane-evaluations one launch processes, on average (SURVEY.md §8(d) units) ...
     launch_evals = {"k_precheck": 8 * single.ctMPUs / nparts, "k_mpu": 512 * fmpus / launches,
                     "k_vertex": 4 * single.ctVertices / nparts, "k_finish": 4 * single.ctVertices / nparts}
+    launch_evals["k_front"] = launch_evals["k_precheck"] + launch_evals["k_mpu"]
     # ... times the fp32 ops per lane-evaluation of that stage that the reference executes on
     # this input (its own op-box pruning included; the oracle's counters priced by
     # parsip_amd/costmodel.py, tests/golden/workload_ops.json); else the unpruned figure
     wops = workload_ops(args.config) if scaling == "weak" or grp.world == 1 else None
-    per_eval, per_src = costmodel.ops_per_eval(model), "costmodel.ops_per_eval (unpruned tree)"
-    if wops and wops.get("vertices") == single.ctVertices and dom in wops:
-        ref_evals = {"k_precheck": 8 * mine.ctMPUs, "k_mpu": 512 * wops["passed_s1"],
-                     "k_vertex": 4 * wops["vertices"], "k_finish": 4 * wops["vertices"]}[dom]
-        per_eval, per_src = wops[dom] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
-    alg_ops = launch_evals[dom] * per_eval
+    unpruned = costmodel.ops_per_eval(model)
+
+    def eval_price(k):  # fp32 ops per lane-evaluation of stage k, and where the figure comes from
+        if wops and wops.get("vertices") == single.ctVertices and k in wops:
+            ref_evals = {"k_precheck": 8 * mine.ctMPUs, "k_mpu": 512 * wops["passed_s1"],
+                         "k_vertex": 4 * wops["vertices"], "k_finish": 4 * wops["vertices"]}[k]
+            return wops[k] / ref_evals, "tests/golden/workload_ops.json (reference-executed ops per eval)"
+        return unpruned, "costmodel.ops_per_eval (unpruned tree)"
+    if dom == "k_front":  # S1's and S2's evaluations, each at its stage's price
+        (pp, per_src), (pm, _) = eval_price("k_precheck"), eval_price("k_mpu")
+        alg_ops = launch_evals["k_precheck"] * pp + launch_evals["k_mpu"] * pm
+        per_eval = alg_ops / launch_evals["k_front"]
+    else:
+        per_eval, per_src = eval_price(dom)
+        alg_ops = launch_evals[dom] * per_eval
     # the launch duration: hipEvent pairs on the engine's stream in the timed regime (the
     # contract's measure; it agrees with rocprofv3's mean for the same command), the
     # device-clock span of the replay beside it
@@ -769,7 +793,8 @@ def main():
             "lane_evals": round(launch_evals[dom]),
             "ops_per_eval": round(per_eval, 1), "ops_per_eval_source": per_src, "algorithmic_ops": round(alg_ops),
             "note": "per launch: achieved = the lane-evaluations one launch performs (k_mpu: 512 x S2-evaluated "
-                    "MPUs of its part) x the reference's fp32 ops per evaluation / its duration in the timed "
+                    "MPUs of its part; k_front: k_precheck's 8 per MPU + k_mpu's, each at its stage's price) x "
+                    "the reference's fp32 ops per evaluation / its duration in the timed "
                     "regime (engines alternating, queued: the launches of the other engines share the CUs); "
                     "'isolated' is the same launch with the device to itself. Exact per-wave "
                     "culling skips part of those ops, so valu_issue (executed VALU instructions x 2 cycles per "
@@ -778,7 +803,8 @@ def main():
     lk["kernels_ms"] = {k: {"span": round(kt[k], 4), "hipevent": round(ev_ms.get(k, 0.0), 4),
                               "isolated": round(solo.get(k, 0.0), 4)} for k in kt}
     if dom in solo:
-        solo_evals = dict(launch_evals, k_mpu=512 * solo_fm / solo_n)[dom]
+        solo_evals = dict(launch_evals, k_mpu=512 * solo_fm / solo_n,
+                          k_front=launch_evals["k_precheck"] + 512 * solo_fm / solo_n)[dom]
         a_solo = solo_evals * per_eval / (solo[dom] * 1e-3) / 1e12
         lk["isolated"] = {"kernel_ms": round(solo[dom], 4), "achieved": round(a_solo, 3),
                             "frac": round(a_solo / NOFMA_PEAK_TOPS, 4),
@@ -807,7 +833,7 @@ def main():
     step = None
     if pmc and prof_ok:
         ks = {k: v for k, v in pmc.items() if "SQ_INSTS_VALU" in v and "probe" not in k}
-        first = profile_entry(pmc, "k_precheck", timed_jit)
+        first = profile_entry(pmc, "k_precheck", timed_jit) or profile_entry(pmc, "k_front", timed_jit)
         steps_prof = (first or {}).get("launches")
         if ks and steps_prof:
             instr = sum(v["SQ_INSTS_VALU"] * v.get("launches", steps_prof) for v in ks.values()) / steps_prof
@@ -815,7 +841,7 @@ def main():
             issue = instr * 2 / (sec * 2.4e9 * 1024)
             lane_tops = instr * 64 / sec / 1e12
             tr_step = None
-            tfirst = profile_entry(tr, "k_precheck", timed_jit) if tr else None
+            tfirst = (profile_entry(tr, "k_precheck", timed_jit) or profile_entry(tr, "k_front", timed_jit)) if tr else None
             if tfirst and tfirst.get("calls"):  # launches per step from the kernel-trace call counts
                 tr_step = sum(v.get("traffic_bytes", 0.0) * v.get("calls", tfirst["calls"]) / tfirst["calls"]
                               for k, v in tr.items() if "probe" not in k)
@@ -872,8 +898,11 @@ def main():
                    "grids": "k_vertex / k_finish: a wave per batch of the last run's vertices + 1/8, at most "
                             "the persistent grids" if os.environ.get("PSGPU_GRID_FIT", "1") != "0" else "persistent",
                    "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
-                   "step": "one complete polygonization of the rank's MPU range (all four kernels); steps "
-                           "alternate between the engines and are queued without host sync",
+                   "step": "one complete polygonization of the rank's MPU range (S1-S6: k_precheck + k_mpu, "
+                           "one launch when launch_flags says k_front, then k_vertex + k_finish, or k_surface); "
+                           "steps alternate between the engines and are queued without host sync",
+                   "launch_flags": {"k_front": front, "tree_split": bool(mine.launchFlags & gpu.LAUNCH_TREE_SPLIT),
+                                    "k_surface": bool(mine.launchFlags & gpu.LAUNCH_SURFACE)},
                    "mpu_range_rank0": [begin, end] if grp.rank == 0 else None,
                    "exchange": exchange, "culling": not args.no_cull, "tree_split": args.tree_split,
                    "fused_surface": ("auto: k_vertex + k_finish as one launch when both take their quad layouts"

@@ -369,9 +369,11 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        compiled with PSGPU_OPT_TREE_SPLIT != 0.  Identical output */
 #define PSGPU_OPT_FRONT        22   /* k_precheck + k_mpu as one launch, S1 survivors handed to the
                                        S2 blocks of the same launch as they are published (no grid
-                                       barrier): 0 (default) two launches, 1 always (with the
-                                       generated kernels), 2 for the tree-split small launches;
-                                       env PSGPU_FRONT; never with PSGPU_OPT_MPU_TICKS */
+                                       barrier): 0 two launches, 1 always (generated kernels),
+                                       2 (default) when k_precheck's grid is at most 8 blocks per
+                                       CU (C3 and its shares, not C5's 512^3 frame); env
+                                       PSGPU_FRONT; never with PSGPU_OPT_MPU_TICKS, nor while
+                                       more than 3 other contexts have runs pending on the device */
 #define PSGPU_OPT_MPU_TICKS    19   /* 1: runs record per-MPU ticks for MPUSTATS
                                        (psgpu_download_process_stats); 0 (default) off */
 #define PSGPU_OPT_JIT_ASYNC    11   /* 1 (default): set_model returns at once; hiprtc compiles the

@@ -490,15 +490,20 @@ bool use_split(const psgpu_ctx* c) {
     return c->treeSplit == 1 || (c->treeSplit == 2 && c->haveQueued && c->lastQueued <= c->splitMaxQueued);
 }
 
-// k_precheck + k_mpu as one launch (k_front) for the next run: 1 forces it, 2 for the split
-// kernels' small launches (use_split); never with per-MPU ticks (MPUSTATS: S1 and S2 would
-// write an MPU's tick words from two XCDs in one launch) or while finish re-runs a run whose
-// in-kernel wait gave up (surfaceOff)
+// k_precheck + k_mpu as one launch (k_front) for the next run: 1 forces it, 2 (default) when
+// the k_precheck grid is at most 8 blocks per CU -- C3 and its rank shares, whose step the
+// boundary and the S1 tail weigh on (the driver's C3 window -7 %, one engine -2.4 %), not C5's
+// 512^3 frame (13 k S1 blocks: +4.6 %, the fused kernel's registers cost its S1 waves a slot;
+// profiles/r06_front_ab.txt).  Never with per-MPU ticks (MPUSTATS: S1 and S2 would write an
+// MPU's tick words from two XCDs in one launch), on a crowded device, or while finish re-runs a
+// run whose in-kernel wait gave up (surfaceOff).
 bool use_front(const psgpu_ctx* c) {
-    if (!c->jit || c->front == 0 || c->surfaceOff || c->mpuTicksOpt) return false;
+    if (!c->jit || c->front == 0 || c->surfaceOff || c->crowded || c->mpuTicksOpt) return false;
     const bool split = use_split(c);
     if (!(split ? c->jit->frontS : c->jit->front)) return false;
-    return c->front == 1 || split;
+    if (c->front == 1) return true;
+    const size_t mpb = split ? 2u : (size_t)kMpusPerBlock;
+    return (brick_count(c) + mpb - 1) / mpb <= 8u * (size_t)c->numCUs;
 }
 
 Params make_params(psgpu_ctx* c) {
@@ -619,7 +624,7 @@ int vertex_vpw(const psgpu_ctx* c) {
 // both would take their quad layouts (a launch too small to fill the device: its step is the
 // launch floor); only with the small-launch kernels (compiled with the split)
 bool use_surface(const psgpu_ctx* c) {
-    if (!c->jit || !c->jit->surface || c->fusedSurface == 0 || c->surfaceOff) return false;
+    if (!c->jit || !c->jit->surface || c->fusedSurface == 0 || c->surfaceOff || c->crowded) return false;
     return c->fusedSurface == 1 || (vertex_vpw(c) == 16 && finish_vpw(c) == 16 && c->lastV != 0);
 }
 
@@ -756,6 +761,7 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
 // the layouts with the shortest spans; runs that overlap other contexts' (contexts taking
 // frames in turn) take the layouts with the least total work.
 std::atomic<int> g_pendingRuns[64];
+constexpr int kMaxWaitingPeers = 4;  // see psgpu_polygonize: crowded
 void set_pending(psgpu_ctx* c, bool v) {
     if (c->pending == v) return;
     c->pending = v;
@@ -1291,7 +1297,15 @@ int psgpu_polygonize(psgpu_ctx* c, float cellsize, uint32_t mpuBegin, uint32_t m
     if (rc != PSGPU_RET_SUCCESS) return rc;
     // alone: no OTHER context has a run pending on the device (this context's own earlier
     // runs share its stream, so they never overlap this one)
-    c->alone = g_pendingRuns[c->device & 63].load() - (c->pending ? 1 : 0) == 0;
+    const int others = g_pendingRuns[c->device & 63].load() - (c->pending ? 1 : 0);
+    c->alone = others == 0;
+    // the launches with in-kernel waits (k_surface, k_front) only while at most 3 other contexts
+    // of the process have runs in flight on the device: with more, the waiting blocks of all
+    // their launches can hold every slot of an XCD that another launch's awaited blocks still
+    // need (blocks go to the XCDs round-robin, each XCD dispatching its share in order), and the
+    // waits end only at their bounds (6-8 engines on a C4 share: protocol errors, ms per step;
+    // profiles/r06_engines_waits.txt)
+    c->crowded = others >= kMaxWaitingPeers;
     rc = enqueue(c, s);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     c->runStream = s;
@@ -1773,6 +1787,7 @@ bool ScatterJob::wait_piece(int k) {
                     }
                     break;
                 }
+                if (trace) tPiece[n] = now_ns();
                 ready.store(++n, std::memory_order_release);
             }
             polling.store(false, std::memory_order_release);
@@ -1820,6 +1835,10 @@ bool ScatterJob::range(uint32_t lb, uint32_t le, int* have) {
 // the range), in ascending order, so the pieces are waited for in the order they come
 void ScatterJob::task(unsigned k, unsigned nth) {
     if (!active) return;
+    if (trace) {
+        int64_t z = 0;
+        (void)tFirstTask.compare_exchange_strong(z, now_ns());
+    }
     int have = 0;
     const uint32_t N = (uint32_t)S->N;
     for (uint32_t b = k * 128u; b < N; b += nth * 128u)
@@ -1877,20 +1896,54 @@ int scatter_jobs(psgpu_ctx* c, ScatterJob* jobs, size_t n) {
     return PSGPU_RET_SUCCESS;
 }
 
-int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats) {
+// PSGPU_EXPORT_TRACE=1: every blocking export prints its phases (ms from the call's start) to
+// stderr -- kernels done, packing enqueued, metadata in, first scatter task, each piece in,
+// scatter done, end (tools/blocking_seq.py collects them)
+bool export_trace_on() {
+    static const bool on = [] {
+        const char* e = getenv("PSGPU_EXPORT_TRACE");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
+bool prewake_on() {
+    static const bool on = [] {
+        const char* e = getenv("PSGPU_PREWAKE");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
+int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats, const int64_t* tr) {
     ScatterJob job;
+    job.trace = tr != nullptr;
     int rc = job.prepare(c, S, mpus);
+    const int64_t tPrep = tr ? now_ns() : 0;
     if (rc == PSGPU_RET_SUCCESS) rc = scatter_jobs(c, &job, 1);
+    const int64_t tScat = tr ? now_ns() : 0;
     if (rc == PSGPU_RET_SUCCESS) rc = job.finish(stats);
+    if (tr) {
+        const int64_t t0 = tr[0], tEnd = now_ns();
+        auto ms = [t0](int64_t t) { return t ? (double)(t - t0) * 1e-6 : -1.0; };
+        fprintf(stderr, "psgpu export: mpus %zu V %zu pieces %d | kernels %.3f packing %.3f meta %.3f first_task %.3f pieces",
+                S.N, S.V, S.pieces, ms(tr[1]), ms(tr[2]), ms(tPrep), ms(job.tFirstTask.load()));
+        for (int k = 0; k < S.pieces; ++k) fprintf(stderr, " %.3f", ms(job.tPiece[k]));
+        fprintf(stderr, " | scatter %.3f end %.3f\n", ms(tScat), ms(tEnd));
+    }
     return rc;
 }
 }  // namespace psgpu
 
 namespace {
-int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt, PsMpuStats* stats) {
+int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outCt, PsMpuStats* stats,
+                    int64_t tCall = 0) {
+    int64_t tr[3] = {tCall ? tCall : now_ns(), 0, 0};
+    const bool trace = export_trace_on();
     PsMeshInfo I;
     int rc = psgpu_finish(c, &I);
     if (rc != PSGPU_RET_SUCCESS) return rc;
+    tr[1] = now_ns();
     if (outCt) *outCt = c->mpuCount;
     if (mpus) {
         if (c->mpuCount > capacity) return PSGPU_RET_MPU_OVERFLOW;
@@ -1900,7 +1953,8 @@ int export_blocking(psgpu_ctx* c, PsMPU* mpus, uint32_t capacity, uint32_t* outC
     ExportStage st;
     rc = export_stage(c, mpus != nullptr, stats != nullptr, &st);
     if (rc != PSGPU_RET_SUCCESS) return rc;
-    return export_scatter(c, st, mpus, stats);
+    tr[2] = now_ns();
+    return export_scatter(c, st, mpus, stats, trace ? tr : nullptr);
 }
 }  // namespace
 
@@ -1924,6 +1978,7 @@ int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* pr
                           PsMpuStats* stats) {
     if (!c || !prims) return PSGPU_RET_PARAM_ERROR;
     if (prims->ctPrims == 0) return PSGPU_RET_PARAM_ERROR;  // Polygonize :322-323
+    const int64_t tCall = now_ns();
     int rc = psgpu_set_model(c, prims, mats, ops);
     if (rc != PSGPU_RET_SUCCESS) return rc;
     rc = psgpu_polygonize(c, cellsize, 0, 0xffffffffu, nullptr);
@@ -1932,7 +1987,9 @@ int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* pr
         rc = psgpu_export_polympus(c, nullptr, capacity, outCt);
         return rc;
     }
-    return export_blocking(c, mpus, capacity, outCt, stats);
+    // the scatter threads start spinning while the kernels run (they sleep between calls)
+    if (c->scatterPool && prewake_on()) c->scatterPool->prewake();
+    return export_blocking(c, mpus, capacity, outCt, stats, tCall);
 }
 
 int psgpu_polygonize_mpus_ex(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* prims, const PsSoaPrimMatrices* mats,

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -53,6 +54,8 @@ struct psgpu_ctx {
     // this run enqueued while no other run of the process was pending on the device (a
     // blocking caller): the layout defaults pick the shorter-span (latency) layouts
     bool alone = false;
+    // ... or while 4 or more other contexts have runs pending on it: no in-kernel waits then
+    bool crowded = false;
     // PSGPU_OPT_JIT 3 (tiered): once the model has stayed unchanged for tierRuns runs, its
     // baked kernels compile on a host thread and replace the structure kernels (kept in jit1)
     int tier = 0;                      // what `jit` holds: 0 none, 1 structure, 2 baked kernels
@@ -73,7 +76,7 @@ struct psgpu_ctx {
     bool splittable = false;  // the model's walk splits at the root (jit_splittable)
     int fusedSurface = 2;     // PSGPU_OPT_FUSED_SURFACE: k_vertex + k_finish in one launch (use_surface)
     bool runSurface = false;  // the last enqueued run took k_surface
-    int front = 0;            // PSGPU_OPT_FRONT: k_precheck + k_mpu in one launch (use_front)
+    int front = 2;            // PSGPU_OPT_FRONT: k_precheck + k_mpu in one launch (use_front)
     bool runFront = false;    // the last enqueued run took k_front
     bool runSplit = false;    // ... and the tree-split kernels
     uint32_t lastSubMax = 0;  // the largest k_front sub-queue of the last finished run (0: none)
@@ -185,7 +188,12 @@ struct ExportStage {
 // `after`: an event the packing kernel waits for (the previous part's packing on the same
 // device, so the parts' pieces cross the link in range order)
 int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_t after = nullptr);
-int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats);
+int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats, const int64_t* trace = nullptr);
+bool export_trace_on();
+bool prewake_on();  // PSGPU_PREWAKE=0: the scatter threads are not woken ahead of the export (A/B)
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 // One staged export's scatter into PolyMPUs, split so that a group's parts go in one pass of
 // the thread pool (scatter_jobs): prepare (after the metadata), task per thread, finish.
 struct ScatterJob {
@@ -203,6 +211,11 @@ struct ScatterJob {
     size_t pbase[kExportPieces] = {}, pv0[kExportPieces] = {}, pt0[kExportPieces] = {}, pnv[kExportPieces] = {};
     int prepare(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus);
     std::atomic<int> ready{0};        // pieces known to be in (-1: the packing kernel failed)
+    // PSGPU_EXPORT_TRACE: steady-clock ns when the first scatter task started, when each piece
+    // was seen in (export_blocking prints the call's phases to stderr)
+    bool trace = false;
+    std::atomic<int64_t> tFirstTask{0};
+    int64_t tPiece[kExportPieces] = {};
     std::atomic<bool> polling{false};  // a thread is reading the flags
     bool wait_piece(int k);
     bool range(uint32_t lb, uint32_t le, int* have);

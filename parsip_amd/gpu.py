@@ -624,9 +624,9 @@ class Group:
         """Per-kernel hipEvent times (ms) of part `part` in the last finished run."""
         return _kernel_times(self._L, ctypes.c_void_p(self.context_ptr(part)))
 
-    def spans(self, part: int) -> np.ndarray:
-        """Recorded kernel spans (OPT_SPANS) of part `part`: (runs, kernels) in ms."""
-        return _spans(self._L, ctypes.c_void_p(self.context_ptr(part)))
+    def spans(self, part: int, raw: bool = False) -> np.ndarray:
+        """Recorded kernel spans (OPT_SPANS) of part `part`: (runs, kernels) in ms (raw: start / end ticks)."""
+        return _spans(self._L, ctypes.c_void_p(self.context_ptr(part)), raw)
 
     def stamps(self, part: int) -> dict:
         """The per-wave timeline (OPT_STAMPS) of part `part` in the last finished run."""
@@ -656,13 +656,18 @@ def _spans(L, ctx, raw: bool = False) -> np.ndarray:
     return (out[:, :, 1] - out[:, :, 0]) * 1e-5  # (runs, kernels) in ms (100 MHz ticks)
 
 
-def kernel_spans(stamps: dict) -> dict:
-    """Per kernel, first wave start -> last wave end (ms, device clock) of one run."""
+def kernel_spans(stamps: dict, front: bool = False) -> dict:
+    """Per kernel, first wave start -> last wave end (ms, device clock) of one run; front: the
+    run's S1 and S2 waves were one launch (k_front, PsMeshInfo.launchFlags), whose span is added."""
     out = {}
     for k in STAMP_KERNELS:
         st = stamps.get(k)
         if st is not None and len(st):
             out[k] = float(int(st[:, 1].max()) - int(st[:, 0].min())) * 1e-5  # 100 MHz ticks -> ms
+    if front:
+        st = [stamps[k] for k in ("k_precheck", "k_mpu") if stamps.get(k) is not None and len(stamps[k])]
+        if st:
+            out["k_front"] = float(max(int(x[:, 1].max()) for x in st) - min(int(x[:, 0].min()) for x in st)) * 1e-5
     return out
 
 

@@ -54,6 +54,6 @@ def test_fuzz_ranges_and_trees(gpu_poly, oracle, seed):
         gpu_poly.set_option(gpu.OPT_FINISH_QUAD, 2)
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
         gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
-        gpu_poly.set_option(gpu.OPT_FRONT, 0)
+        gpu_poly.set_option(gpu.OPT_FRONT, 2)
     om = oracle.polygonize(model, cs, begin, end, threads=8)
     assert_mesh_matches(gm, gs, om)

@@ -264,7 +264,7 @@ def test_front_golden(gpu_poly, name, split):
     finally:
         gpu_poly.set_option(gpu.OPT_DEBUG, 0)
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
-        gpu_poly.set_option(gpu.OPT_FRONT, 0)
+        gpu_poly.set_option(gpu.OPT_FRONT, 2)
 
 
 def test_front_protocol_error_reruns(gpu_poly, capfd):
@@ -294,7 +294,7 @@ def test_front_protocol_error_reruns(gpu_poly, capfd):
     finally:
         gpu_poly.set_option(gpu.OPT_DEBUG, 0)
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
-        gpu_poly.set_option(gpu.OPT_FRONT, 0)
+        gpu_poly.set_option(gpu.OPT_FRONT, 2)
 
 
 def test_engines_pipelined_c3_golden():
