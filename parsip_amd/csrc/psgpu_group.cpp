@@ -497,8 +497,6 @@ int psgpu_group_polygonize_mpus(psgpu_group* g, float cellsize, const PsSoaBlobP
     if (rc != PSGPU_RET_SUCCESS) return rc;
     rc = psgpu_group_polygonize(g, cellsize);
     if (rc != PSGPU_RET_SUCCESS) return rc;
-    // the scatter threads start spinning while the kernels run (they sleep between calls)
-    if (mpus && !g->parts.empty() && g->parts[0]->scatterPool && prewake_on()) g->parts[0]->scatterPool->prewake();
     return psgpu_group_export_polympus(g, mpus, capacity, outCt);
 }
 

@@ -1669,7 +1669,7 @@ int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_
     // words only ever hold flags (an older call's epoch, or 0), never mesh or offset words, so
     // no stale word can equal this call's epoch (r04 kept them behind the mesh, where a call
     // with a smaller mesh found the previous call's packed triangles and offsets -- ADVICE r04)
-    const size_t flagBytes = 4 * (size_t)kExportPieces * kExportPackBlocks;
+    const size_t flagBytes = 4 * (size_t)kExportPieces * kExportPackBlocks * kExportFlagStride;
     S.oFlags = 0;
     S.oOffs = up(flagBytes);
     S.oPass = up(S.oOffs + (N + 1) * 8);
@@ -1771,16 +1771,20 @@ bool ScatterJob::wait_piece(int k) {
         if (polling.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
             int n = ready.load(std::memory_order_acquire);
             while (n >= 0 && n < S->pieces) {  // advance over every piece already in
-                const uint32_t* f = flags + (size_t)n * S->packBlocks;
-                uint32_t b = 0;
-                while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
+                const uint32_t* f = flags + (size_t)n * S->packBlocks * kExportFlagStride;
+                // from the first flag not yet seen up: every read of a flag still down is a read
+                // of a line the device is about to write (one flag a line, kExportFlagStride)
+                uint32_t b = pollBlock;
+                while (b < S->packBlocks && __atomic_load_n(f + (size_t)b * kExportFlagStride, __ATOMIC_ACQUIRE) == S->epoch) ++b;
+                pollBlock = b;
                 if (b < S->packBlocks) {
                     if ((spin & 63) == 0) {
                         const hipError_t e = hipEventQuery(c->exportEv[1]);
                         if (e != hipErrorNotReady) {  // done (every flag must be up) or failed
-                            while (b < S->packBlocks && __atomic_load_n(f + b, __ATOMIC_ACQUIRE) == S->epoch) ++b;
+                            while (b < S->packBlocks && __atomic_load_n(f + (size_t)b * kExportFlagStride, __ATOMIC_ACQUIRE) == S->epoch) ++b;
                             if (e != hipSuccess || b < S->packBlocks) n = -1;
                             else ++n;
+                            pollBlock = 0;
                             ready.store(n, std::memory_order_release);
                             continue;
                         }
@@ -1788,6 +1792,7 @@ bool ScatterJob::wait_piece(int k) {
                     break;
                 }
                 if (trace) tPiece[n] = now_ns();
+                pollBlock = 0;
                 ready.store(++n, std::memory_order_release);
             }
             polling.store(false, std::memory_order_release);
@@ -1907,14 +1912,6 @@ bool export_trace_on() {
     return on;
 }
 
-bool prewake_on() {
-    static const bool on = [] {
-        const char* e = getenv("PSGPU_PREWAKE");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-
 int export_scatter(psgpu_ctx* c, const ExportStage& S, PsMPU* mpus, PsMpuStats* stats, const int64_t* tr) {
     ScatterJob job;
     job.trace = tr != nullptr;
@@ -1987,8 +1984,6 @@ int psgpu_polygonize_mpus(psgpu_ctx* c, float cellsize, const PsSoaBlobPrims* pr
         rc = psgpu_export_polympus(c, nullptr, capacity, outCt);
         return rc;
     }
-    // the scatter threads start spinning while the kernels run (they sleep between calls)
-    if (c->scatterPool && prewake_on()) c->scatterPool->prewake();
     return export_blocking(c, mpus, capacity, outCt, stats, tCall);
 }
 

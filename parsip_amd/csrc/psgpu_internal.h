@@ -190,7 +190,6 @@ struct ExportStage {
 int export_stage(psgpu_ctx* c, bool mesh, bool stats, ExportStage* st, hipEvent_t after = nullptr);
 int export_scatter(psgpu_ctx* c, const ExportStage& st, PsMPU* mpus, PsMpuStats* stats, const int64_t* trace = nullptr);
 bool export_trace_on();
-bool prewake_on();  // PSGPU_PREWAKE=0: the scatter threads are not woken ahead of the export (A/B)
 inline int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -217,6 +216,7 @@ struct ScatterJob {
     std::atomic<int64_t> tFirstTask{0};
     int64_t tPiece[kExportPieces] = {};
     std::atomic<bool> polling{false};  // a thread is reading the flags
+    uint32_t pollBlock = 0;            // the poller's place in the current piece's flags (under `polling`)
     bool wait_piece(int k);
     bool range(uint32_t lb, uint32_t le, int* have);
     void task(unsigned k, unsigned nth);

@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(64) k_sum_totals(TotalsParts tp, uint32_t* __r
 // The blocking export's packing (psgpu_launch.h PackSrc), written straight into the pinned host
 // staging over PCIe -- no copy-engine transfers (each cost ~13 us of setup, r04) and one launch:
 // every block walks the pieces in order, writes its share of one, then raises its flag for it
-// (flags[piece * gridDim.x + block] = epoch, a system-scope release), so the host scatters
+// (flags[(piece * gridDim.x + block) * kExportFlagStride] = epoch, a system-scope release), so the host scatters
 // piece k while piece k + 1 is still on the link.
 __global__ void __launch_bounds__(256) k_export_pack(PackSrc src, uint32_t* __restrict__ dst) {
     uint64_t base = 0;  // the piece's first word
@@ -138,8 +138,8 @@ __global__ void __launch_bounds__(256) k_export_pack(PackSrc src, uint32_t* __re
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(src.flags + (uint64_t)k * gridDim.x + blockIdx.x, src.epoch, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(src.flags + ((uint64_t)k * gridDim.x + blockIdx.x) * kExportFlagStride, src.epoch,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

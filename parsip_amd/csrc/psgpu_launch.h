@@ -38,12 +38,16 @@ struct PackSrc {
     const float *pos, *nrm, *col;
     const uint32_t* tris;
     uint32_t n, pieces;
-    uint32_t* flags;  // [pieces][blocks], set to epoch as each block finishes a piece
+    uint32_t* flags;  // [pieces][blocks] x kExportFlagStride words, set to epoch as each block finishes a piece
     uint32_t epoch, blocks;
     uint32_t delayBlock;  // test hook (PSGPU_OPT_DEBUG bit 24): this block waits delayTicks of the
     uint32_t delayTicks;  // 100 MHz device clock before each piece's share (0xffffffff: none)
 };
 constexpr uint32_t kExportPackBlocks = 256;
+// every block's flag on a 64-B line of its own: the host's poller, re-reading the line of the
+// first flag still down, then shares it with no other block's flag write (16 flags a line made
+// some calls' whole transfer ~5x slower: DESIGN.md §4 "Blocking", profiles/r06_blocking_tail.txt)
+constexpr uint32_t kExportFlagStride = 16;
 hipError_t launch_export_pack(const PackSrc& src, uint32_t* dst, hipStream_t s);
 struct MetaSrc {  // offs / counts null when not exported
     const uint64_t* offs;

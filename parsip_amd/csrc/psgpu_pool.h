@@ -78,17 +78,6 @@ public:
     }
     ~ScatterPool() { stop_all(); }
     unsigned workers() const { return (unsigned)th_.size(); }
-    // Wake the sleeping workers now, ahead of a job that will come within ~spinUs (a blocking
-    // call does this before its kernels run): the job then finds them spinning instead of paying
-    // the futex wake-ups and the scheduler's latency of 16 threads when it is ready (the tail of
-    // calls that came after the workers had gone to sleep, DESIGN.md §4 "Blocking").
-    void prewake() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            wake_.fetch_add(1, std::memory_order_release);
-        }
-        cv_.notify_all();
-    }
 
     // callerDrains: the calling thread takes tasks too (false: it only waits -- when the
     // workers are pinned to a node the caller may not be on)
@@ -132,35 +121,28 @@ private:
         }
     }
     void work() {
-        uint32_t seen = 0, woken = wake_.load(std::memory_order_acquire);
+        uint32_t seen = 0;
         for (;;) {
-            // a short spin for the next job (back-to-back calls, or a prewake), then sleep
+            // a short spin for the next job (back-to-back calls), then sleep
             const auto t0 = std::chrono::steady_clock::now();
             while ((uint32_t)(state_.load(std::memory_order_acquire) >> 32) == seen &&
-                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs))
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
                 std::this_thread::yield();
-            if ((uint32_t)(state_.load(std::memory_order_acquire) >> 32) == seen) {
+            {
                 std::unique_lock<std::mutex> l(mu_);
-                cv_.wait(l, [&] {
-                    return stop_ || (uint32_t)(state_.load(std::memory_order_acquire) >> 32) != seen ||
-                           wake_.load(std::memory_order_acquire) != woken;
-                });
+                cv_.wait(l, [&] { return stop_ || (uint32_t)(state_.load(std::memory_order_acquire) >> 32) != seen; });
                 if (stop_) return;
-                woken = wake_.load(std::memory_order_acquire);
-                if ((uint32_t)(state_.load(std::memory_order_acquire) >> 32) == seen) continue;  // prewake: spin
             }
             seen = (uint32_t)(state_.load(std::memory_order_acquire) >> 32);
             drain(seen);
         }
     }
-    static constexpr int kSpinUs = 500;  // a C3 call's kernels and packing start take ~0.15 ms
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
     const std::function<void(unsigned)>* f_ = nullptr;
     std::atomic<uint64_t> state_{0};  // job << 32 | count << 16 | next
     std::atomic<uint32_t> left_{0};
-    std::atomic<uint32_t> wake_{0};
     uint32_t gen_ = 0;
     bool stop_ = false;
 };
