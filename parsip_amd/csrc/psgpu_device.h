@@ -151,6 +151,9 @@ __device__ __forceinline__ uint32_t lane_value(uint32_t v, int lane) {
 // A value the wave holds in every lane, as a scalar (SGPR): branches on it are scalar, and
 // the compiler sees the uniformity its divergence analysis cannot prove (e.g. anything
 // derived from threadIdx.x >> 6).
+#ifndef PSGPU_DEFER_ATOMICS
+#define PSGPU_DEFER_ATOMICS 1  // 0: wait for the queue reservations' atomics where they return (A/B)
+#endif
 #ifndef PSGPU_UNIFORM_CM
 #define PSGPU_UNIFORM_CM 1  // 0: k_mpu's culling mask in VGPRs (experiments)
 #endif
@@ -1000,24 +1003,16 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
     // choice only) at pq + q * fqCap, its count in shard q's p; otherwise the brick's shard
     const uint32_t qsel = FRONT ? (blockIdx.x & 7u) : shard;
     const uint32_t qbase = FRONT ? qsel * p.fqCap : shard * p.pShardCap;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&p.ctr->shard[qsel].p, (uint32_t)__popc(queue8));
-    base = lane_value(base, 0);
-    if (pass) {
-        const uint32_t slotq = qbase + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
-        if (FRONT) __hip_atomic_store(&p.pq[slotq], mOf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-        else p.pq[slotq] = mOf;
-        // the MPU's octants proven uniform by the same bounds: k_mpu evaluates only the others
-        // (their inside bits are the proof's), bits 0-7 all outside, 8-15 all inside
-        if (PSGPU_S2_OCT)
-            p.pqOct[slotq] = (uint16_t)(((octOut >> (8 * lane)) & 0xffull) | (((octIn >> (8 * lane)) & 0xffull) << 8));
-    }
-    phase_stamp(p, 3, 8192u);
+    // the queue reservation's returning atomic is waited for only after the culling masks are
+    // made (their round trip overlaps the mask computation; verdict r05 item 4)
+    uint32_t baseAtomic = 0;
+    if (lane == 0) baseAtomic = atomicAdd(&p.ctr->shard[qsel].p, (uint32_t)__popc(queue8));
     // Culling mask of each queued MPU, from this wave's culling segments (already in
     // registers): its box grown by the normal delta, for k_vertex / k_finish (mpuMasks) and,
     // with the queue entry, for S2 (k_mpu loads no culling data).  The grown box contains the
     // S2 box, so its mask is conservative there too; one mask per MPU instead of two (the
     // boxes differ by 0.001: the masks are the same but for primitives grazing the box).
+    uint64_t mLo = 0ull, mHi = 0ull;  // lane q < 8: MPU q's mask, for its queue entry
     if (p.cull) {
         const float eg = 7.0f * p.cs + 0.001f;
         for (uint32_t qm = queue8; qm != 0u; qm &= qm - 1u) {
@@ -1026,21 +1021,40 @@ __device__ __forceinline__ void precheck_body(const Params& p, float* lds) {
             const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[1]), 8 * q));
             const float oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[2]), 8 * q));
             const CullMask g = cull_mask_from(cl, ox, oy, oz, ox + eg, oy + eg, oz + eg);
-            const uint32_t slotq = qbase + base + (uint32_t)__popc(queue8 & ((1u << q) - 1u));
             const uint32_t wq = lane_value(mOf, q) - p.mpuBegin;
             if (lane == 0) {
-                if (FRONT) {  // read in this launch by S2 waves on other CUs: write-through (sc1)
-                    __hip_atomic_store(&p.pqMask[2 * slotq], g.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&p.pqMask[2 * slotq + 1], g.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    p.pqMask[2 * slotq] = g.lo;
-                    p.pqMask[2 * slotq + 1] = g.hi;
-                }
                 p.mpuMasks[2 * wq] = g.lo;
                 p.mpuMasks[2 * wq + 1] = g.hi;
             }
+            if (lane == q) {
+                mLo = g.lo;
+                mHi = g.hi;
+            }
         }
     }
+    if (PSGPU_DEFER_ATOMICS) asm volatile("" : "+v"(baseAtomic) : "v"(mLo));  // the wait for the atomic goes here
+    const uint32_t base = lane_value(baseAtomic, 0);
+    if (pass) {  // lane q < 8 writes MPU q's entry
+        const uint32_t slotq = qbase + base + (uint32_t)__popc(queue8 & ((1u << lane) - 1u));
+        if (FRONT) {  // read in this launch by S2 waves on other CUs: write-through (sc1)
+            __hip_atomic_store(&p.pq[slotq], mOf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (p.cull) {
+                __hip_atomic_store(&p.pqMask[2 * slotq], mLo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&p.pqMask[2 * slotq + 1], mHi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            p.pq[slotq] = mOf;
+            if (p.cull) {
+                p.pqMask[2 * slotq] = mLo;
+                p.pqMask[2 * slotq + 1] = mHi;
+            }
+        }
+        // the MPU's octants proven uniform by the same bounds: k_mpu evaluates only the others
+        // (their inside bits are the proof's), bits 0-7 all outside, 8-15 all inside
+        if (PSGPU_S2_OCT)
+            p.pqOct[slotq] = (uint16_t)(((octOut >> (8 * lane)) & 0xffull) | (((octIn >> (8 * lane)) & 0xffull) << 8));
+    }
+    phase_stamp(p, 3, 8192u);
     if constexpr (FRONT) {
         // publish (MI355X_MICROARCH.md hand-off table, first row): the entries and masks were
         // stored sc1; once they have left this wave (vmcnt(0)), each queued MPU's ready word
@@ -1403,6 +1417,10 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // Every wave of the MPU computes V and T; the first writes the tables and counters.
     const uint64_t edgeBits = tab->edge;
     uint32_t V = 0, T = 0;
+    // WPM 1: the record queues' bases stay in lane 0's registers (the returning atomics are not
+    // waited for until pass 2 stores its first record: their round trip overlaps the record's
+    // cell search; verdict r05 item 4: the record passes hold half of k_mpu's parked cycles)
+    uint32_t qvAtomic = 0u, qtAtomic = 0u;
     if (work) {
         uint32_t carry = 0;  // V | T << 16 (both <= 343 * 12 per MPU: no carry between the halves)
         const int j = lane >> 3, k = lane & 7;
@@ -1436,8 +1454,12 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
         if (part == 0) {
             const uint32_t shard = d & (kShards - 1);
             if (lane == 0) {
-                sQ[0] = atomicAdd(&p.ctr->shard[shard].v, V);
-                sQ[1] = atomicAdd(&p.ctr->shard[w & (kShards - 1)].t, T);  // TriRec: shard = w & 63
+                qvAtomic = atomicAdd(&p.ctr->shard[shard].v, V);
+                qtAtomic = atomicAdd(&p.ctr->shard[w & (kShards - 1)].t, T);  // TriRec: shard = w & 63
+                if (WPM > 1) {
+                    sQ[0] = qvAtomic;
+                    sQ[1] = qtAtomic;
+                }
                 p.counts[w] = (uint64_t)V | ((uint64_t)T << 32);
                 if (T > 0) atomicAdd(&p.ctr->shard[shard].s, 1u);
                 if (V > 512u || T > 512u) atomicMin(&p.ctr->firstOverflow, (int)m);
@@ -1465,7 +1487,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
     // k-th owned crossing edge in first-occurrence order of the row, k = r - first id.
     // Records are written coalesced.
     if (recs) {
-        const uint32_t qv = sQ[0];
+        uint32_t qv = WPM > 1 ? sQ[0] : 0u;
         for (uint32_t b0 = (uint32_t)part * 64u; b0 < V; b0 += 64u * WPM) {
             const uint32_t r = b0 + (uint32_t)lane;
             if (r < V) {
@@ -1488,6 +1510,11 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
                 const int sx = i + ((c1 >> 2) & 1), sy = j + ((c1 >> 1) & 1), sz = k + (c1 & 1);
                 edgeVid[((sx * 8 + sy) * 8 + sz) * 3 + ax] = (uint16_t)r;
                 const uint32_t key = (uint32_t)sx | ((uint32_t)sy << 3) | ((uint32_t)sz << 6) | ((uint32_t)ax << 9);
+                if (WPM == 1) {  // lane 0's atomic result, read only once the record is made (the
+                                 // empty asm ties the read, and the wait for the atomic, to the key)
+                    if (PSGPU_DEFER_ATOMICS) asm volatile("" : "+v"(qvAtomic) : "v"(key));
+                    qv = lane_value(qvAtomic, 0);
+                }
                 const uint32_t g = qv + r;
                 if (g < p.vShardCap) vk[g] = VertexKey{w, r | (key << 16)};
             }
@@ -1499,7 +1526,7 @@ __device__ __forceinline__ void mpu_body(const Params& p, unsigned char* smem, u
 
     // pass 3 (S6, :816-825), one lane per triangle r: its cell (last first-id <= r) and
     // the (r - first)-th triangle of the cell's table row
-    const uint32_t qt = sQ[1];
+    const uint32_t qt = WPM > 1 ? sQ[1] : lane_value(qtAtomic, 0);
     for (uint32_t b0 = (uint32_t)part * 64u; b0 < T; b0 += 64u * WPM) {
         const uint32_t r = b0 + (uint32_t)lane;
         if (r < T) {

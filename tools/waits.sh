@@ -27,6 +27,7 @@ done
 echo "pass 2 counters:$P2"
 for V in "s|--jit 1|0" "b|--jit 2|0" "s1|--jit 1|1" "s32|--jit 1|32"; do
   IFS='|' read -r name args dbg <<< "$V"
+  mkdir -p $OUT/$name
   i=0
   for SET in "${SETS[@]}"; do
     i=$((i+1))
