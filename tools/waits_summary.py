@@ -4,7 +4,7 @@ wave and, where the counters exist, how long an instruction of each class stays 
 (LEVEL / INSTS, cycles); then the parked cycles the variants remove:
   structure - baked       = waits on the per-primitive scalar parameter loads (lgkmcnt);
   s - s1 (k_mpu)          = waits in the record passes (LDS / table loads, barriers);
-  s - s32 (vertex/finish) = waits inside the walks (parameters, culling masks);
+  s - s32 (k_finish)      = waits inside the walks (parameters, culling masks);
 what stays in s32 is the records' / keys' / offsets' vector loads and stores (vmcnt) and the
 block barriers.  Usage: python tools/waits_summary.py gpurun_out/<tag> [> table]"""
 import json
@@ -57,7 +57,7 @@ for k in names:
         a["scalar_parameter_loads"] = g["s"] - g["b"]
     if "s1" in g and k == "jit_mpu":
         a["record_passes"] = g["s"] - g["s1"]
-    if "s32" in g and k in ("jit_vertex", "jit_vertex_w", "jit_finish", "jit_finish_p", "jit_finish_q"):
+    if "s32" in g and k in ("jit_finish", "jit_finish_p", "jit_finish_q"):  # bit 5 ablates k_finish's walks only
         a["walks"] = g["s"] - g["s32"]
         a["records_offsets_stores_barriers"] = g["s32"]
     attr[k] = {n: (round(x / g["s"], 3) if n != "parked_total" else round(x)) for n, x in a.items()}
