@@ -365,8 +365,11 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
 #define PSGPU_OPT_FUSED_SURFACE 21  /* k_vertex + k_finish as one launch (quad layouts, the offsets
                                        scan released inside it): 2 (default) for runs whose last
                                        run's vertices take the quad layouts in both (small rank
-                                       shares), 1 always, 0 never.  Needs the small-launch kernels,
-                                       compiled with PSGPU_OPT_TREE_SPLIT != 0.  Identical output */
+                                       shares), 1 always, 0 never, 3 always with one lane per
+                                       vertex for both walks (k_surface_w: full grids; measured
+                                       within 1-2 % of the two launches, so not a default).  Needs
+                                       the small-launch kernels, compiled with
+                                       PSGPU_OPT_TREE_SPLIT != 0.  Identical output */
 #define PSGPU_OPT_FRONT        22   /* k_precheck + k_mpu as one launch, S1 survivors handed to the
                                        S2 blocks of the same launch as they are published (no grid
                                        barrier): 0 two launches, 1 always (generated kernels),

@@ -2308,7 +2308,10 @@ __device__ __forceinline__ uint64_t surface_offs(const Params& p, uint32_t i) {
 // before its first mesh write.  Same values as the two kernels: the same expressions on the
 // same records and the same culling masks.  The scan blocks have the lowest block ids, so they
 // are dispatched before any waiting block of their XCD: the wait cannot starve them.
-template <class EV>
+// VPW 64 (k_surface_w, PSGPU_OPT_FUSED_SURFACE 3): one lane per vertex for both walks -- the root's
+// 4 edge samples as k_vertex's wide layout walks them, then value + colour and the 3 normal samples
+// as k_finish's 64-vertex layout -- for launches whose vertices fill the device.
+template <class EV, int VPW = 16>
 __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
     const int wave = wave_index();
     const int lane = lane_id();
@@ -2363,6 +2366,85 @@ __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
     stage_shard_counts(p, 2, sCnt + kShards);  // ShardCtr::t
     __syncthreads();
     bool scanSeen = blockIdx.x == 0;  // block 0 waited above
+if constexpr (VPW == 64) {
+    const ShardBatches sw(sCnt, p.vShardCap, 64);
+    for (uint32_t batch = wave0; batch < sw.total; batch += nWaves) {
+        uint32_t shard, first, count;
+        sw.locate(batch, &shard, &first, &count);
+        uint32_t rec = first + (uint32_t)lane;
+        const bool valid = rec < count;
+        if (!valid) rec = first;
+        const size_t ri = (size_t)shard * p.vShardCap + rec;
+        const VertexKey K = p.vk[ri];
+        const EdgeSeg E = edge_segment(p, K.w, K.vidKey >> 16);
+        // the root: the lane's 4 edge samples as one 4-point walk (vertex_body, 64 per wave)
+        float xs[4], ys[4], zs[4], fs[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            xs[s2] = edge_sample(E.e[0], E.d[0], s2);
+            ys[s2] = edge_sample(E.e[1], E.d[1], s2);
+            zs[s2] = edge_sample(E.e[2], E.d[2], s2);
+        }
+        CullMask cmv{0ull, 0ull};
+        if (p.cull) cmv = cull_mask_mpus(p, K.w);
+        if (p.debug & 256u) {  // ablation bit 8: no phase-A walk
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) fs[s2] = xs[s2];
+        } else {
+            ev.template evaln<0, false, 4>(xs, ys, zs, cmv, fs, nullptr);
+        }
+        const bool st0 = fs[0] >= 0.5f;
+        const int iv = ((fs[1] >= 0.5f) != st0) ? 1 : (((fs[2] >= 0.5f) != st0) ? 2 : 3);
+        const float fa = iv == 1 ? fs[0] : (iv == 2 ? fs[1] : fs[2]);
+        const float fb = iv == 1 ? fs[1] : (iv == 2 ? fs[2] : fs[3]);
+        const float scale = (0.5f - fa) / (fb - fa);
+        // value, colour and normal at the root (finish_body, 64 per wave)
+        float P[3];
+        vertex_root(E, (uint32_t)iv, scale, P);
+        const bool onSeg = scale >= 0.0f && scale <= 1.0f;
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        if (!(p.debug & 32u)) {  // ablation bit 5: no walks
+            CullMask cm{0ull, 0ull};
+            if (p.cull) {
+                if (ballot(!onSeg) == 0ull) cm = cmv;  // cull_mask_mpus(p, K.w), as just made
+                else cm = cull_mask_points(M, P[0], P[1], P[2], true, delta);
+            }
+            const float qx[4] = {P[0], P[0] + delta, P[0], P[0]};
+            const float qy[4] = {P[1], P[1], P[1] + delta, P[1]};
+            const float qz[4] = {P[2], P[2], P[2], P[2] + delta};
+            float g[4], c4[12];
+            ev.template evaln<1, true, 4>(qx, qy, qz, cm, g, c4);
+            c[0] = c4[0];
+            c[1] = c4[1];
+            c[2] = c4[2];
+            const float vtx = g[0];
+            nx = (g[1] - vtx) * inv;
+            ny = (g[2] - vtx) * inv;
+            nz = (g[3] - vtx) * inv;
+            const float im = 1.0f / sqrtf((nx * nx + ny * ny) + nz * nz);
+            nx = nx * im;
+            ny = ny * im;
+            nz = nz * im;
+        }
+        if (!scanSeen) {
+            surface_wait_scan(p);
+            scanSeen = true;
+        }
+        const uint32_t gi = (uint32_t)surface_offs(p, K.w) + (K.vidKey & 0xffffu);
+        if (valid && gi < p.vCap) {  // past vCap: finish() grows and re-runs
+            p.pos[gi * 3 + 0] = P[0];
+            p.pos[gi * 3 + 1] = P[1];
+            p.pos[gi * 3 + 2] = P[2];
+            p.nrm[gi * 3 + 0] = nx;
+            p.nrm[gi * 3 + 1] = ny;
+            p.nrm[gi * 3 + 2] = nz;
+            p.col[gi * 3 + 0] = c[0];
+            p.col[gi * 3 + 1] = c[1];
+            p.col[gi * 3 + 2] = c[2];
+        }
+    }
+} else {
     const ShardBatches sv(sCnt, p.vShardCap, 16);
     const int qj = lane & 3;
     for (uint32_t batch = wave0; batch < sv.total; batch += nWaves) {
@@ -2430,6 +2512,7 @@ __device__ __forceinline__ void surface_body(const Params& p, float* lds) {
             p.col[o] = qj == 0 ? c[0] : (qj == 1 ? c[1] : c[2]);
         }
     }
+}
     if (p.debug & 64u) return;  // ablation bit 6: no triangles
     const ShardBatches sb(sCnt + kShards, p.tShardCap, 64);
     if (wave0 < sb.total && !scanSeen) surface_wait_scan(p);

@@ -625,6 +625,7 @@ int vertex_vpw(const psgpu_ctx* c) {
 // launch floor); only with the small-launch kernels (compiled with the split)
 bool use_surface(const psgpu_ctx* c) {
     if (!c->jit || !c->jit->surface || c->fusedSurface == 0 || c->surfaceOff || c->crowded) return false;
+    if (c->fusedSurface == 3) return c->jit->surfaceW != nullptr;  // the wide variant, every launch
     return c->fusedSurface == 1 || (vertex_vpw(c) == 16 && finish_vpw(c) == 16 && c->lastV != 0);
 }
 
@@ -664,12 +665,14 @@ int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {
         gridF = std::min<uint32_t>(gridF, (uint32_t)((vv + 4ull * vpw - 1) / (4ull * vpw)));
     }
     if (use_surface(c)) {  // both quad layouts in one launch: the vertex grid (16 per wave)
-        uint32_t gridS = std::max(persistV, p.scanBlocks);
+        const bool wide = c->fusedSurface == 3;  // or one lane per vertex: k_finish's grid (64 per wave)
+        const uint32_t perBlock = wide ? 256u : 64u;
+        uint32_t gridS = std::max(wide ? persistF : persistV, p.scanBlocks);
         if (c->gridFit && c->lastV) {
             const uint64_t vv = (uint64_t)c->lastV + c->lastV / 8 + 256;
-            gridS = std::max(p.scanBlocks, std::min<uint32_t>(gridS, (uint32_t)((vv + 63ull) / 64ull)));
+            gridS = std::max(p.scanBlocks, std::min<uint32_t>(gridS, (uint32_t)((vv + perBlock - 1) / perBlock)));
         }
-        PSGPU_CHECK(launch_jit(J->surface, gridS, 256, 0, s, p));
+        PSGPU_CHECK(launch_jit(wide ? J->surfaceW : J->surface, gridS, 256, 0, s, p));
         if (timed) {
             PSGPU_CHECK(hipEventRecord(c->ev[3], s));
             PSGPU_CHECK(hipEventRecord(c->ev[4], s));
@@ -1103,7 +1106,7 @@ int psgpu_create(int deviceOrdinal, psgpu_ctx** out) {
     if (const char* e = getenv("PSGPU_FINISH_QUAD")) c->finishQuad = std::min(3, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_VERTEX_WIDE")) c->vertexWide = std::min(2, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_MPU_MARGIN")) c->mpuMarginDiv = std::max(1, atoi(e));
-    if (const char* e = getenv("PSGPU_FUSED_SURFACE")) c->fusedSurface = std::min(2, std::max(0, atoi(e)));
+    if (const char* e = getenv("PSGPU_FUSED_SURFACE")) c->fusedSurface = std::min(3, std::max(0, atoi(e)));
     if (const char* e = getenv("PSGPU_FRONT")) c->front = std::min(2, std::max(0, atoi(e)));
     *out = c;
     return PSGPU_RET_SUCCESS;
@@ -1181,7 +1184,7 @@ int psgpu_set_option(psgpu_ctx* c, int option, int64_t value) {
         }
     }
     else if (option == PSGPU_OPT_SPLIT_MAX_QUEUED && value >= 0 && value <= 0xffffffffll) c->splitMaxQueued = (uint32_t)value;
-    else if (option == PSGPU_OPT_FUSED_SURFACE && value >= 0 && value <= 2) c->fusedSurface = (int)value;
+    else if (option == PSGPU_OPT_FUSED_SURFACE && value >= 0 && value <= 3) c->fusedSurface = (int)value;
     else if (option == PSGPU_OPT_FRONT && value >= 0 && value <= 2) c->front = (int)value;
     else if (option == PSGPU_OPT_TIER_RUNS && value >= 1 && value <= (1 << 30)) c->tierRuns = (int)value;
     else if (option == PSGPU_OPT_JIT) {

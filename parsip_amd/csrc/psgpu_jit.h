@@ -17,6 +17,7 @@ struct JitKernels {
                   finishQ = nullptr, finishP = nullptr, probe = nullptr;
     hipFunction_t precheckS = nullptr, mpuS = nullptr;  // tree split at the root (two waves per item)
     hipFunction_t surface = nullptr;  // k_vertex + k_finish in one launch (small launches; with the split kernels)
+    hipFunction_t surfaceW = nullptr;  // the same with one lane per vertex (PSGPU_OPT_FUSED_SURFACE 3)
     hipFunction_t front = nullptr, frontS = nullptr;  // k_precheck + k_mpu in one launch (k_front; unsplit / split)
 };
 

@@ -159,10 +159,12 @@ def test_fused_surface_golden(gpu_poly, name):
     try:
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 1)
         gpu_poly.jit_wait()  # the split option compiles the small-launch kernels
-        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 1)
-        for _ in range(2):
-            gpu_poly.run(cs)
-            assert digest() == dig
+        for mode in (1, 3):  # the quad and the one-lane-per-vertex k_surface
+            gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, mode)
+            for _ in range(2):
+                info = gpu_poly.run(cs)
+                assert info.launchFlags & gpu.LAUNCH_SURFACE
+                assert digest() == dig, mode
         b = gpu_poly.plan_split(cs, 8)
         lo, hi = int(b[3]), int(b[4])
         got = {}
