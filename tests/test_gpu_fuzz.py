@@ -40,7 +40,7 @@ def test_fuzz_ranges_and_trees(gpu_poly, oracle, seed):
         gpu_poly.set_option(gpu.OPT_FINISH_QUAD, fquad)
         front = (seed // 2) % 3  # k_front (with the small-launch kernels: split 0 compiles them as 2)
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, (split if split or not front else 2) if jit else 0)
-        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, seed % 3)  # k_surface when the split compiled it
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, seed % 4)  # k_surface (3: k_surface_w) when the split compiled it
         gpu_poly.set_option(gpu.OPT_FRONT, front)
         gpu_poly.set_model(model)
         assert gpu_poly.jit_active == bool(jit)
