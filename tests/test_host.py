@@ -189,6 +189,10 @@ def test_generated_kernels_resources():
     # reads of the vertex and triangle passes (surface_offs); k_vertex has the look-back's only
     assert ks["jit_surface"]["load_x2_sc1"] >= 3, ks["jit_surface"]
     assert ks["jit_vertex"]["load_x2_sc1"] >= 1, ks["jit_vertex"]
+    # k_front's hand-off (MI355X_MICROARCH.md's table, first row) needs every byte stored and loaded
+    # sc1: entry, the mask's two words and the ready word on each side, and the poll loads
+    for k in ("jit_front", "jit_front_s"):
+        assert ks[k]["store_sc1"] >= 4 and ks[k]["load_sc1"] >= 5 and ks[k]["load_x2_sc1"] >= 2, (k, ks[k])
 
 
 _JIT_TREES = r"""

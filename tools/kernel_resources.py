@@ -63,7 +63,7 @@ def instruction_mix(co: str) -> dict:
         if m:
             cur = m.group(1)
             mix[cur] = {"instructions": 0, "valu": 0, "s_nop": 0, "s_waitcnt": 0, "v_pk_fp32": 0, "dpp": 0,
-                        "code_bytes": 0, "load_x2_sc1": 0}
+                        "code_bytes": 0, "load_x2_sc1": 0, "load_sc1": 0, "store_sc1": 0}
             continue
         if cur is None:
             continue
@@ -82,10 +82,15 @@ def instruction_mix(co: str) -> dict:
                 d["v_pk_fp32"] += 1
             if "_dpp" in op or "row_" in line or "quad_perm" in line:
                 d["dpp"] += 1
-        elif op == "global_load_dwordx2" and re.search(r"\bsc1\b", line.split("//")[0]):
-            # agent-scope 64-bit loads: the offsets-scan look-back and k_surface's offsets reads
-            # (surface_offs), which must bypass the non-coherent caches
-            d["load_x2_sc1"] += 1
+        elif op.startswith("global_load") and re.search(r"\bsc1\b", line.split("//")[0]):
+            # agent-scope loads: the offsets-scan look-back and k_surface's offsets reads
+            # (surface_offs), k_front's entries, masks and ready words -- they must bypass the
+            # non-coherent caches
+            d["load_sc1"] += 1
+            if op == "global_load_dwordx2":
+                d["load_x2_sc1"] += 1
+        elif op.startswith("global_store") and re.search(r"\bsc1\b", line.split("//")[0]):
+            d["store_sc1"] += 1  # write-through stores: k_front's published entries, masks, ready words
         elif op == "s_nop":
             d["s_nop"] += 1
         elif op == "s_waitcnt":
