@@ -1,7 +1,7 @@
 """Long seeded fuzz run of the GPU path against the oracle (the cases of tests/test_gpu_fuzz.py,
 many more seeds): random trees over every node type, matrices, off-round cell sizes, ragged
-MPU ranges, culling on / off, interpreter / generated kernels, every layout, the tree split
-and the fused k_surface.  Prints one line per failure and a summary; exit status 1 if any case differs.
+MPU ranges, culling on / off, interpreter / generated kernels, every layout, the tree split,
+the fused k_surface / k_surface_w and k_front.  Prints one line per failure and a summary; exit status 1 if any case differs.
 
 Usage (GPU): python tools/fuzz_parity.py [--first 0] [--count 400] [--big]
 (--big: trees of 25-64 primitives; the generated kernels on every fourth case, the
@@ -47,8 +47,10 @@ def main():
         poly.set_option(gpu.OPT_JIT, jit)
         poly.set_option(gpu.OPT_VERTEX_WIDE, vwide)
         poly.set_option(gpu.OPT_FINISH_QUAD, fquad)
-        poly.set_option(gpu.OPT_TREE_SPLIT, split if jit else 0)
-        poly.set_option(gpu.OPT_FUSED_SURFACE, seed % 3)  # k_surface when the split compiled it
+        front = (seed // 2) % 3  # k_front (with the small-launch kernels: split 0 compiles them as 2)
+        poly.set_option(gpu.OPT_TREE_SPLIT, (split if split or not front else 2) if jit else 0)
+        poly.set_option(gpu.OPT_FUSED_SURFACE, seed % 4)  # k_surface (3: k_surface_w) when the split compiled it
+        poly.set_option(gpu.OPT_FRONT, front)
         poly.set_model(model)  # waits for the generated kernels when jit is on
         assert poly.jit_active == bool(jit), seed
         poly.run(cs, begin, end)
