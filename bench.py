@@ -714,8 +714,11 @@ def main():
     if front:  # the hipEvent pair before / after the one launch ("k_precheck"; "k_mpu" brackets nothing)
         ev_ms["k_front"] = ev_ms.pop("k_precheck", 0.0)
         ev_ms.pop("k_mpu", None)
+    fused = int(os.environ.get("PSGPU_FUSED_SURFACE", "2"))
     for e in engines:
         e.set_option(gpu.OPT_STAMPS, 1 << 17)
+        if fused == 2:  # the timed regime's launches: a lone run would otherwise fuse k_vertex + k_finish
+            e.set_option(gpu.OPT_FUSED_SURFACE, 1 if mine.launchFlags & gpu.LAUNCH_SURFACE else 0)
     # the same launches with the device to themselves (engine 0 alone): the per-kernel
     # figure without the other engine's kernels sharing the CUs
     solo_sum, solo_n, solo_fm = {}, 0, 0
@@ -728,6 +731,8 @@ def main():
             solo_n += 1
     for e in engines:
         e.set_option(gpu.OPT_STAMPS, 0)
+        if fused == 2:
+            e.set_option(gpu.OPT_FUSED_SURFACE, 2)
     solo = {k: v / solo_n for k, v in solo_sum.items()}
     single = mine
     # the dominant kernel: the longest launch with the device to itself (the replay spans of

@@ -626,7 +626,13 @@ int vertex_vpw(const psgpu_ctx* c) {
 bool use_surface(const psgpu_ctx* c) {
     if (!c->jit || !c->jit->surface || c->fusedSurface == 0 || c->surfaceOff || c->crowded) return false;
     if (c->fusedSurface == 3) return c->jit->surfaceW != nullptr;  // the wide variant, every launch
-    return c->fusedSurface == 1 || (vertex_vpw(c) == 16 && finish_vpw(c) == 16 && c->lastV != 0);
+    // a run alone on the device (a blocking caller, a frame-at-a-time editor) is bound by its
+    // spans: the quad layouts in one launch, while their waves fill the device at most ~8 times
+    // (C3 alone 0.110 vs 0.115 ms; C5's 512^3 frame, far more vertices, 0.613 vs 0.600:
+    // profiles/r06_latency_ab.txt)
+    const uint64_t loneMaxV = 16ull * 8ull * 24ull * (uint64_t)c->numCUs;  // 16 a wave, 24 waves a CU, 8 passes
+    return c->fusedSurface == 1 ||
+           (c->lastV != 0 && ((c->alone && c->lastV <= loneMaxV) || (vertex_vpw(c) == 16 && finish_vpw(c) == 16)));
 }
 
 int launch_all(psgpu_ctx* c, const Params& pin, hipStream_t s, bool timed) {

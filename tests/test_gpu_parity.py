@@ -24,6 +24,8 @@ def run_both(poly, oracle, model, cs, begin=0, end=None, cull=1, jit=1, vwide=2,
     poly.set_option(gpu.OPT_JIT, jit)
     poly.set_option(gpu.OPT_VERTEX_WIDE, vwide)
     poly.set_option(gpu.OPT_TREE_SPLIT, split)
+    # a forced k_vertex layout must run k_vertex (a lone run otherwise takes k_surface)
+    poly.set_option(gpu.OPT_FUSED_SURFACE, 2 if vwide == 2 else 0)
     poly.set_model(model)
     assert poly.jit_active == bool(jit)
     poly.run(cs, begin, end)
@@ -79,6 +81,7 @@ def test_finish_layouts_golden(gpu_poly, name, jit):
     dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
     model, cs, _ = synth.make_config(name)
     gpu_poly.set_option(gpu.OPT_JIT, jit)
+    gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 0)  # k_finish itself (a lone run would take k_surface)
     gpu_poly.set_model(model)
     try:
         for mode in (0, 1, 3, 2, 2):
@@ -89,6 +92,7 @@ def test_finish_layouts_golden(gpu_poly, name, jit):
             assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig, (name, jit, mode)
     finally:
         gpu_poly.set_option(gpu.OPT_FINISH_QUAD, 2)
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
         gpu_poly.set_option(gpu.OPT_JIT, 1)
 
 
@@ -102,6 +106,7 @@ def test_vertex_layouts_golden(gpu_poly, name, jit):
     dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))[name]
     model, cs, _ = synth.make_config(name)
     gpu_poly.set_option(gpu.OPT_JIT, jit)
+    gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 0)  # k_vertex itself (a lone run would take k_surface)
     gpu_poly.set_model(model)
     try:
         for mode in (0, 1, 2, 2):
@@ -112,6 +117,7 @@ def test_vertex_layouts_golden(gpu_poly, name, jit):
             assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig, (name, jit, mode)
     finally:
         gpu_poly.set_option(gpu.OPT_VERTEX_WIDE, 2)
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
         gpu_poly.set_option(gpu.OPT_JIT, 1)
 
 
@@ -380,6 +386,7 @@ def test_random_trees(gpu_poly, oracle, seed, layout):
     finally:
         gpu_poly.set_option(gpu.OPT_VERTEX_WIDE, 2)
         gpu_poly.set_option(gpu.OPT_TREE_SPLIT, 0)
+        gpu_poly.set_option(gpu.OPT_FUSED_SURFACE, 2)
     assert_mesh_matches(gm, gs, om)
 
 
