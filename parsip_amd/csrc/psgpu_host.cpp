@@ -856,6 +856,11 @@ void tier_count(psgpu_ctx* c) {
 void jit_start(psgpu_ctx* c) {
     c->jit.reset();
     c->jit1.reset();
+    // a compile still running for the previous model or options finishes in the background, and
+    // psgpu_destroy waits for it: a hiprtc thread left running into process exit can outlive
+    // the compiler's own lazily built statics (a core dump after a run that changed options
+    // under a compile, tools/fuzz_parity.py in round 6)
+    if (c->jitPending && c->jitFut.valid()) c->retired.push_back(c->jitFut);
     c->jitPending = false;
     c->jitFut = JitFuture();
     c->tier = 0;
