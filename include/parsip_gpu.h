@@ -312,7 +312,10 @@ int  psgpu_set_option(psgpu_ctx* ctx, int option, int64_t value);
                                        after a few polls; either way finish sees the protocol
                                        error and re-runs the polygonization as separate
                                        launches (k_precheck, k_mpu, k_vertex, k_finish; a
-                                       second error: -6) */
+                                       second error: -6);
+                                       bit 28 (test hook): the next run starts 3 runs short of
+                                       the run counter's 32-bit wrap, where the context
+                                       restarts its counter sets at epoch 0 */
 #define PSGPU_OPT_VERTEX_BLOCKS_PER_CU 4  /* persistent k_vertex grid, 256-thread blocks per CU; once a
                                              run of the same range has finished, the grid is fitted
                                              to its vertices (+1/8) up to this (env PSGPU_GRID_FIT=0:

@@ -716,6 +716,20 @@ int enqueue(psgpu_ctx* c, hipStream_t s) {
         PSGPU_CHECK(hipMemcpyAsync(c->totals, c->emptyTotals, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         return PSGPU_RET_SUCCESS;
     }
+    if (c->debug & (1 << 28)) {  // test hook: 3 runs short of the epoch's wrap
+        c->debug &= ~(1 << 28);
+        reset_run_state(c);
+        DevCounters near;
+        PSGPU_CHECK(hipMemcpy(&near, c->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost));
+        near.epoch = 0xfffffffcu;
+        PSGPU_CHECK(hipMemcpy(c->ctr, &near, sizeof(DevCounters), hipMemcpyHostToDevice));
+        c->epochRuns = near.epoch;
+    }
+    // a run at epoch 0xffffffff would tag k_front's entries 0, the value of ready words no run
+    // has written: restart the counter sets at epoch 0 with the ready words zeroed (a stream
+    // drain once in 2^32 runs)
+    if (c->epochRuns >= 0xffffffffull) reset_run_state(c);
+    ++c->epochRuns;
     const Params p = make_params(c);
     c->runTicks = p.mpuTicks != nullptr;
     c->debug &= ~((1 << 20) | (1 << 25) | (1 << 26) | (1 << 27));  // the short-grid / protocol test hooks apply to one run
@@ -894,6 +908,7 @@ void reset_run_state(psgpu_ctx* c) {
     if (c->fqReady) (void)hipMemset(c->fqReady, 0, c->capFq * sizeof(uint32_t));  // the epochs restart at 0
     (void)hipDeviceSynchronize();
     c->parity = 0;
+    c->epochRuns = 0;
     drop_graphs(c);
 }
 

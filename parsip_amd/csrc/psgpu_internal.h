@@ -114,6 +114,9 @@ struct psgpu_ctx {
     uint32_t runMpuBlocks = 0;      // k_mpu grid of the last enqueued run
     uint64_t* scanStatus = nullptr; // 2 x kScanMaxBlocks look-back words (alternating runs)
     uint32_t parity = 0;            // which counter / status set the next run uses
+    // runs launched since the counter sets last started at epoch 0 = the next run's epoch
+    // (DevCounters::epoch; k_front tags its queue entries epoch + 1, which must never wrap to 0)
+    uint64_t epochRuns = 0;
     uint64_t* counts = nullptr;
     uint8_t* passed = nullptr;      // per MPU: passed S1
     size_t capPassed = 0;

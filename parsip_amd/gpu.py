@@ -91,6 +91,7 @@ LAUNCH_TREE_SPLIT, LAUNCH_SURFACE, LAUNCH_FRONT, LAUNCH_RERUN = 1, 2, 4, 8  # Ps
 DEBUG_SURFACE_LATE_SCAN = 1 << 25  # test hooks of the in-kernel waits (OPT_DEBUG bits, one run each)
 DEBUG_LOOKBACK_TIMEOUT = 1 << 26
 DEBUG_FRONT_LATE_S1 = 1 << 27
+DEBUG_EPOCH_NEAR_WRAP = 1 << 28  # test hook: the next run starts 3 runs short of the epoch's wrap
 DEBUG_EXPORT_POISON = 1 << 23  # test hooks of the blocking export (OPT_DEBUG bits)
 DEBUG_EXPORT_STRAGGLER = 1 << 24
 JIT_INTERP, JIT_STRUCTURE, JIT_BAKED, JIT_TIERED = 0, 1, 2, 3  # OPT_JIT values

@@ -305,6 +305,31 @@ def test_front_protocol_error_reruns(gpu_poly, capfd):
         gpu_poly.set_option(gpu.OPT_FRONT, 2)
 
 
+def test_front_epoch_wrap(gpu_poly):
+    """k_front tags its queue entries with the run's epoch + 1 and takes an entry whose ready word
+    holds that tag; at epoch 0xffffffff the tag would be 0, the value of every ready word no run
+    has written.  Hook (debug bit 28): the context starts 3 runs short of the wrap; the runs up
+    to it and the ones after the context restarts its counter sets at epoch 0 all reproduce the
+    C2 oracle digests."""
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    dig = json.load(open(os.path.join(gdir, "oracle_digests.json")))["C2"]
+    model, cs, _ = synth.make_config("C2")
+    gpu_poly.set_model(model)
+    try:
+        gpu_poly.set_option(gpu.OPT_FRONT, 1)
+        gpu_poly.run(cs)
+        gpu_poly.set_option(gpu.OPT_DEBUG, gpu.DEBUG_EPOCH_NEAR_WRAP)
+        for k in range(5):  # epochs 0xfffffffc, 0xfffffffd, 0xfffffffe, then 0, 1
+            info = gpu_poly.run(cs)
+            assert info.launchFlags & gpu.LAUNCH_FRONT and not info.launchFlags & gpu.LAUNCH_RERUN, k
+            gm, gs = gpu_poly.download(), gpu_poly.stats()
+            st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]], axis=1)
+            assert mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) == dig, k
+    finally:
+        gpu_poly.set_option(gpu.OPT_DEBUG, 0)
+        gpu_poly.set_option(gpu.OPT_FRONT, 2)
+
+
 def test_engines_pipelined_c3_golden():
     """The bench's pipelining: 4 contexts take 12 C3 polygonizations in turn, queued without
     host synchronisation (bench.py's timed loop); every context's last mesh equals the
