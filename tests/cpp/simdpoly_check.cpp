@@ -21,6 +21,10 @@
 //        thread id and ticks are classes with private members, as legacy TBB's tbb_thread::id
 //        and tbb::tick_count; writes rc, ctMPUs, the host clock (CLOCK_REALTIME ns) before and
 //        after the call, then the ctMPUs 32-byte records.
+//   soa-mt <soa.bin> <cellsize> <out.bin>
+//        4 host threads call PS::SIMDPOLY::Polygonize 3 times each, each into its own PolyMPUs
+//        (each thread runs on its own default context); writes every call's rc, ctMPUs and a
+//        hash of the filled records, PrintThreadResults(3, ...)'s entries, then thread 0's MPUs.
 #include <time.h>
 
 #include <cstdio>
@@ -30,6 +34,7 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mock_blobtree.hpp"
@@ -228,7 +233,7 @@ int main(int argc, char** argv) {
         o.write(reinterpret_cast<const char*>(tris.data()), (std::streamsize)(tris.size() * 4));
         return re == PSGPU_RET_SUCCESS ? 0 : 68;
     }
-    if ((mode == "soa" || mode == "soa-stats" || mode == "soa-threads") && argc >= 5) {
+    if ((mode == "soa" || mode == "soa-stats" || mode == "soa-threads" || mode == "soa-mt") && argc >= 5) {
         static PS::SIMDPOLY::SOABlobPrims prims;
         static PS::SIMDPOLY::SOABlobPrimMatrices mats;
         static PS::SIMDPOLY::SOABlobOps ops;
@@ -278,6 +283,46 @@ int main(int argc, char** argv) {
             o.write(reinterpret_cast<const char*>(cr.data()), (std::streamsize)n * 4);
             o.write(reinterpret_cast<const char*>(pr2.data()), 16);
             o.write(reinterpret_cast<const char*>(poly->vMPUs), (std::streamsize)poly->ctMPUs * sizeof(PsMPU));
+            return 0;
+        }
+        if (mode == "soa-mt") {  // kThreads host threads, kCalls Polygonize each into its own PolyMPUs
+            constexpr int kThreads = 4, kCalls = 3;
+            std::vector<std::unique_ptr<PS::SIMDPOLY::PolyMPUs>> outs;
+            outs.push_back(std::move(poly));
+            for (int t = 1; t < kThreads; ++t) outs.emplace_back(new PS::SIMDPOLY::PolyMPUs());
+            std::vector<int> rcs(kThreads * kCalls, -100);
+            std::vector<uint32_t> cts(kThreads * kCalls, 0u);
+            std::vector<uint64_t> sums(kThreads * kCalls, 0ull);
+            std::vector<std::thread> ts;
+            for (int t = 0; t < kThreads; ++t) {
+                ts.emplace_back([&, t] {
+                    for (int k = 0; k < kCalls; ++k) {
+                        const int i = t * kCalls + k;
+                        rcs[i] = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *outs[t]);
+                        cts[i] = outs[t]->ctMPUs;
+                        // FNV-1a over the filled records' words (the rest of each record is the
+                        // zero of the value-initialised PolyMPUs in every thread)
+                        const uint64_t* w = reinterpret_cast<const uint64_t*>(outs[t]->vMPUs);
+                        uint64_t h = 1469598103934665603ull;
+                        for (size_t j = 0, n = (size_t)cts[i] * sizeof(PsMPU) / 8; j < n; ++j)
+                            h = (h ^ w[j]) * 1099511628211ull;
+                        sums[i] = h;
+                    }
+                });
+            }
+            for (std::thread& t : ts) t.join();
+            const int n = psgpu_thread_result_count();
+            std::vector<uint32_t> pr(n > 0 ? n : 1, 0xdeadbeefu), cr(n > 0 ? n : 1, 0xdeadbeefu);
+            PS::SIMDPOLY::PrintThreadResults(kCalls, pr.data(), cr.data());
+            std::ofstream o(argv[4], std::ios::binary);
+            put(o, kThreads * kCalls);
+            o.write(reinterpret_cast<const char*>(rcs.data()), (std::streamsize)rcs.size() * 4);
+            o.write(reinterpret_cast<const char*>(cts.data()), (std::streamsize)cts.size() * 4);
+            o.write(reinterpret_cast<const char*>(sums.data()), (std::streamsize)sums.size() * 8);
+            put(o, n);
+            o.write(reinterpret_cast<const char*>(pr.data()), (std::streamsize)n * 4);
+            o.write(reinterpret_cast<const char*>(cr.data()), (std::streamsize)n * 4);
+            o.write(reinterpret_cast<const char*>(outs[0]->vMPUs), (std::streamsize)outs[0]->ctMPUs * sizeof(PsMPU));
             return 0;
         }
         const int rc = PS::SIMDPOLY::Polygonize(cs, prims, mats, ops, *poly, NULL);  // the reference's default

@@ -32,7 +32,7 @@ def exe(tmp_path_factory):
     gpu.load()
     out = tmp_path_factory.mktemp("cpp") / "simdpoly_check"
     lib_dir = os.path.join(ROOT, "parsip_amd")
-    subprocess.run([gpp, "-std=c++17", "-O1", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"),
+    subprocess.run([gpp, "-std=c++17", "-O1", "-Wall", "-Wextra", "-pthread", "-I", os.path.join(ROOT, "include"),
                     "-I", os.path.join(ROOT, "tests", "cpp"), os.path.join(ROOT, "tests", "cpp", "simdpoly_check.cpp"),
                     "-L", lib_dir, "-l:libparsip_gpu.so", f"-Wl,-rpath,{lib_dir}", "-o", str(out)], check=True)
     return str(out)
@@ -261,6 +261,47 @@ def test_cpp_ps_simdpoly_print_thread_results(exe, tmp_path):
     assert (pr2 == 0xdeadbeef).all()  # no entry: nothing written
     lines = [l for l in r.stdout.splitlines() if l.startswith("Thread#")]
     assert lines == [f"Thread#  1, Processed MPUs 6859, Crossed MPUs {crossed} "]
+
+
+@pytest.mark.gpu
+def test_cpp_ps_simdpoly_host_threads(exe, tmp_path, oracle):
+    """PS::SIMDPOLY::Polygonize from 4 host threads at once (a host calling the free function
+    from its own workers; each thread runs on its own default context), 3 calls each into its
+    own PolyMPUs: every call succeeds with the same records, thread 0's equal the oracle's, and
+    PrintThreadResults(3, ...) reports one worker per thread with one call's MPUs each."""
+    model, cs, _ = synth.make_config("C2")
+    src, out = tmp_path / "soa.bin", tmp_path / "mt.bin"
+    with open(src, "wb") as f:
+        f.write(model.prims.tobytes() + model.mats.tobytes() + model.ops.tobytes() + model.boxmats.tobytes())
+    r = subprocess.run([exe, "soa-mt", str(src), repr(float(cs)), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(out, "rb").read()
+    calls = int(np.frombuffer(raw[:4], np.int32)[0])
+    at = 4
+    rcs = np.frombuffer(raw[at:at + 4 * calls], np.int32)
+    at += 4 * calls
+    cts = np.frombuffer(raw[at:at + 4 * calls], np.uint32)
+    at += 4 * calls
+    sums = np.frombuffer(raw[at:at + 8 * calls], np.uint64)
+    at += 8 * calls
+    n = int(np.frombuffer(raw[at:at + 4], np.int32)[0])
+    at += 4
+    pr, cr = np.frombuffer(raw[at:at + 8 * n], np.uint32).reshape(2, n)
+    at += 8 * n
+    mpus = np.frombuffer(raw[at:], soa.MPU_DTYPE)
+    assert calls == 12 and (rcs == soa.RET_SUCCESS).all() and (cts == 6859).all()
+    assert len(set(sums.tolist())) == 1, sums
+    om = oracle.polygonize(model, cs, threads=8)
+    np.testing.assert_array_equal(mpus["ctVertices"], om.stats[:, 2])
+    np.testing.assert_array_equal(mpus["ctTriangles"], om.stats[:, 3])
+    for i in np.flatnonzero(om.stats[:, 2]):
+        nv, nt = om.stats[i, 2], om.stats[i, 3]
+        v0, t0 = om.vertex_offsets[i], om.triangle_offsets[i]
+        assert mpus["vPos"][i, :nv * 3].tobytes() == om.pos[v0:v0 + nv].tobytes()
+        np.testing.assert_array_equal(mpus["triangles"][i, :nt * 3].reshape(-1, 3), om.tris[t0:t0 + nt])
+    crossed = int((mpus["ctTriangles"] > 0).sum())
+    assert n == 4 and (pr == 6859).all() and (cr == crossed).all()
 
 
 # ---- compat mode: COMPACTBLOBTREE::convert and CParsipOptimized in C++ (parsip_gpu_gui.hpp)

@@ -354,6 +354,57 @@ def test_engines_pipelined_c3_golden():
             p.close()
 
 
+def test_contexts_on_host_threads():
+    """Four host threads, one context each (a host driving several polygonizers from its own
+    worker threads): ctypes releases the GIL inside the library, so model uploads with their
+    compile requests for the same two trees, polygonizations, finishes and downloads run
+    concurrently; half the threads start on the interpreter while the shared compile is still
+    running.  Every mesh equals its committed oracle digests, and each context's entry of the
+    thread results counts its own runs."""
+    import threading
+
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    digs = json.load(open(os.path.join(gdir, "oracle_digests.json")))
+    runs = 5
+    errors, done = [], []
+
+    def work(i):
+        name = "C2" if i % 2 == 0 else "C3"
+        model, cs, _ = synth.make_config(name)
+        p = gpu.Polygonizer(0)
+        try:
+            p.set_model(model, wait_jit=i < 2)
+            for k in range(runs):
+                p.run(cs)
+                gm, gs = p.download(), p.stats()
+                st = np.stack([gs["passedPrecheck"], gs["ctFieldEvals"], gs["ctVertices"], gs["ctTriangles"]],
+                              axis=1)
+                if mesh_digests(st, gm.pos, gm.nrm, gm.col, gm.local_tris()) != digs[name]:
+                    errors.append((i, k, "digest"))
+            done.append(i)
+        except Exception as e:  # reported by the main thread
+            errors.append((i, repr(e)))
+        finally:
+            p.close()
+
+    gpu.PrintThreadResults(1, echo=False)  # clears the entries of earlier tests
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts), "a host thread did not finish"
+    assert not errors, errors
+    assert sorted(done) == [0, 1, 2, 3]
+    n = gpu.thread_result_count()
+    assert n == 4, n
+    proc, crossed = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+    assert gpu.PrintThreadResults(runs, proc, crossed, echo=False) == 4
+    want = sorted(gpu.count_mpus(c, *m.bbox) for m, c, _ in (synth.make_config(x) for x in ("C2", "C2", "C3", "C3")))
+    assert sorted(proc.tolist()) == want
+    assert (crossed > 0).all() and (crossed < proc).all()
+
+
 def test_engines_different_models_interleaved():
     """Contexts holding different trees (C2, C3: different generated kernels) queued in turn
     without host sync each reproduce their own oracle digests."""
