@@ -17,6 +17,7 @@ from __future__ import annotations
 import atexit
 import ctypes
 import os
+import threading
 import weakref
 from dataclasses import dataclass
 
@@ -492,7 +493,7 @@ def thread_result_count() -> int:
     return int(load().psgpu_thread_result_count())
 
 
-_DEFAULT = {}
+_DEFAULT = threading.local()  # per host thread: {device: Polygonizer}, as parsip_gpu.hpp's default_context()
 
 
 def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None = None, device: int = 0,
@@ -500,16 +501,17 @@ def Polygonize(cellsize: float, model: soa.Model, poly_mpus: np.ndarray | None =
     """Blocking drop-in for PS::SIMDPOLY::Polygonize.
 
     Fills ``poly_mpus`` (a MPU_DTYPE array, default capacity MAX_MPU_COUNT as in PolyMPUs)
-    and returns ``(code, ctMPUs, poly_mpus)``.  Runs on this process's default context of the
+    and returns ``(code, ctMPUs, poly_mpus)``.  Runs on the calling thread's default context of the
     device, as parsip_gpu.hpp's psgpu::Polygonize (a 2-part group's whole call measures the
     same; DESIGN.md §4 "Blocking"); ``stats`` receives per-MPU PsMpuStats, ``process_stats``
     the reference's MPUSTATS (``lpProcessStats``, PS_Polygonizer.h:391).
     """
     if model.ct_prims == 0:
         return soa.RET_PARAM_ERROR, 0, poly_mpus
-    if device not in _DEFAULT:
-        _DEFAULT[device] = Polygonizer(device)
-    return _DEFAULT[device].polygonize_mpus(cellsize, model, poly_mpus, stats, process_stats)
+    mine = _DEFAULT.__dict__.setdefault("polys", {})
+    if device not in mine:
+        mine[device] = Polygonizer(device)
+    return mine[device].polygonize_mpus(cellsize, model, poly_mpus, stats, process_stats)
 
 
 def _mesh_from_arrays(V, T, N, fill):

@@ -576,6 +576,39 @@ def test_drop_in_polygonize(gpu_poly, oracle):
     assert gpu.Polygonize(cs, empty)[0] == soa.RET_PARAM_ERROR
 
 
+def test_drop_in_polygonize_threads(oracle):
+    """gpu.Polygonize from three host threads at once: each thread gets its own default context
+    (as parsip_gpu.hpp's default_context()), every call fills PolyMPUs as the oracle does."""
+    import threading
+
+    model, cs, _ = synth.make_config("C2")
+    om = oracle.polygonize(model, cs, threads=8)
+    res, errors = {}, []
+
+    def work(i):
+        try:
+            for k in range(2):
+                rc, ct, mpus = gpu.Polygonize(cs, model)
+                res[(i, k)] = (rc, ct, mpus["ctVertices"][:ct].copy(), mpus["ctTriangles"][:ct].copy(),
+                               mpus["vPos"][:ct].tobytes())
+        except Exception as e:  # reported by the main thread
+            errors.append((i, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts) and not errors, errors
+    assert len(res) == 6
+    first = res[(0, 0)]
+    for (i, k), (rc, ct, v, t, pos) in res.items():
+        assert rc == soa.RET_SUCCESS and ct == 6859, (i, k)
+        np.testing.assert_array_equal(v, om.stats[:, 2])
+        np.testing.assert_array_equal(t, om.stats[:, 3])
+        assert pos == first[4], (i, k)
+
+
 def test_scene_train(gpu_poly, oracle):
     """The reference's own scene file (95 transformed prims, n-ary ops binarized) through
     the linearizer: matrices on every primitive, Ricci / Difference / Union / Blend."""
